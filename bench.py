@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Benchmark of the quantized-linear hot path on MI355X (BASELINE.json metric).
+
+Default workload (BASELINE.json configs[1]): LLaMA3-8B-shaped int4 group_size=128 dequant-GEMV at
+batch 1 — y[1, 4096] = x[1, 4096] @ W_dq[4096, 4096]^T through the fused gfx950 kernel, over a
+ring of R distinct synthetic matrices (W ~ N(0, 0.02^2), RTN int4 g128 by the build's own HIP
+quantizer; R >= 64 so 563 MB of codes cannot be served by the 256 MB Infinity Cache).
+One step = one pass over the ring (R launches, captured once in a HIP graph and replayed).
+
+Prints ONE JSON line (rank 0).  value = whole-job dequant-matmul TFLOP/s (sum over ranks: every
+rank streams its own ring, no collective in the data path -> weak scaling).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--ring R]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "llama3-quantization_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+MFMA_F16_PEAK_TFS = 2500.0  # dense fp16/bf16 MFMA spec (no sparsity)
+
+WORKLOADS = {
+    # name: (M, N, K, bits, group, ring, kernel, note)
+    "gemv_int4_g128": (1, 4096, 4096, 4, 128, 64, "gemv",
+                       "LLaMA3-8B int4 g128 dequant-GEMV batch=1 (configs[1]), 4096x4096"),
+    "gemv_int3_g64": (1, 4096, 4096, 3, 64, 64, "gemv", "int3 g64 sub-byte GEMV (configs[3])"),
+    "gemv_int2_g64": (1, 4096, 4096, 2, 64, 96, "gemv", "int2 g64 sub-byte GEMV (configs[3])"),
+    "gemm_int4_g128_m32": (32, 4096, 4096, 4, 128, 64, "gemm", "int4 g128, 32 tokens"),
+    "gemm_int4_g128_m2048": (2048, 4096, 4096, 4, 128, 4, "gemm",
+                             "int4 g128, one 2048-token PPL window"),
+    "gemm_int4_g128_m65536": (65536, 4096, 4096, 4, 128, 1, "gemm",
+                              "int4 g128 batch 32 x seq 2048 (configs[2], MFMA path)"),
+}
+
+
+def algo_bytes(M, N, K, bits, group, zero_bytes=1):
+    """2MK + N*K*bits/8 + N*(K/g)*(2 + zb) + 2MN."""
+    return 2 * M * K + N * K * bits // 8 + N * (K // group) * (2 + zero_bytes) + 2 * M * N
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="gemv_int4_g128", choices=sorted(WORKLOADS))
+    ap.add_argument("--ring", type=int, default=None)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(M, N, K, bits, group, seconds):
+    """The reference's fake-quant CPU path, restated by the oracle (numpy), on the host cores.
+
+    Mode (ii) — what the reference runs at eval (weight == W_dq, dense F.linear): x @ W_dq^T over a
+    bounded sample of distinct pre-dequantized matrices (fp32 BLAS), repeated for ~``seconds``.
+    Mode (i) — quantize every call (use_weight_quant=True): oracle.quantize + the same product."""
+    import numpy as np
+    from oracle import quant_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = os.cpu_count() or 1
+    rs = np.random.RandomState(0)
+    nmat = 4
+    mats = []
+    for i in range(nmat):
+        w = (rs.randn(N, K) * 0.02).astype(np.float16)
+        w_dq, *_ = O.quantize(w, bits, group)
+        mats.append(np.ascontiguousarray(w_dq.astype(np.float32)))
+    x = rs.randn(M, K).astype(np.float32)
+    y = mats[0] @ x.T  # warm
+    launches = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for w in mats:
+            y = w @ x.T
+            launches += 1
+    dt = time.perf_counter() - t0
+    tflops = 2.0 * M * N * K * launches / dt / 1e12
+    w16 = (rs.randn(N, K) * 0.02).astype(np.float16)
+    t1 = time.perf_counter()
+    reps = 0
+    while time.perf_counter() - t1 < min(4.0, seconds / 3) or reps == 0:
+        w_dq, *_ = O.quantize(w16, bits, group)
+        y = w_dq.astype(np.float32) @ x.T
+        reps += 1
+    quant_ms = (time.perf_counter() - t1) / reps * 1e3
+    del y
+    return {"value": round(tflops, 6), "unit": "TFLOP/s", "cores": int(threads), "kind": "port",
+            "sample": (f"oracle (numpy fp32 BLAS) x@W_dq^T, M={M} N={N} K={K}, {nmat} distinct "
+                       f"pre-dequantized int{bits} g{group} matrices cycled for {dt:.1f}s "
+                       f"({launches} products; reference eval mode ii)"),
+            "ms_per_product": round(dt / launches * 1e3, 4),
+            "quantize_every_call_ms": round(quant_ms, 2)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from quant import qlin
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    M, N, K, bits, group, ring, kernel, note = WORKLOADS[args.workload]
+    R = args.ring or ring
+    gen = torch.Generator(device=dev)
+    mats = []
+    zb = 1
+    for i in range(R):
+        gen.manual_seed(1_000_003 * rank + i)
+        w = torch.empty(N, K, device=dev, dtype=torch.float16).normal_(0.0, 0.02, generator=gen)
+        o = qlin.quantize(w, bits, group, 0, want_xdq=False, want_params=False, pack=True)
+        z = qlin.narrow_zeros(o["zeros"])
+        zb = z.element_size()
+        mats.append((o["qweight"], o["scales"], z))
+        del w, o
+    gen.manual_seed(1234)
+    x = torch.empty(M, K, device=dev, dtype=torch.float16).normal_(0.0, 1.0, generator=gen)
+    ys = [torch.empty(M, N, device=dev, dtype=torch.float16) for _ in range(min(R, 4))]
+    lib = qlin.load_library()
+    fn = lib.qlin_gemv_f16 if kernel == "gemv" else lib.qlin_gemm_f16
+    zbits = 8 * zb
+
+    def step():
+        st = torch.cuda.current_stream(dev).cuda_stream
+        for i, (qw, sc, z) in enumerate(mats):
+            y = ys[i % len(ys)]
+            if kernel == "gemv":
+                rc = fn(qw.data_ptr(), sc.data_ptr(), z.data_ptr(), zbits, x.data_ptr(), None,
+                        y.data_ptr(), M, N, K, bits, group, st)
+            else:
+                rc = fn(qw.data_ptr(), sc.data_ptr(), z.data_ptr(), zbits, x.data_ptr(), None,
+                        y.data_ptr(), M, N, K, bits, group, None, st)
+            if rc != 0:
+                raise RuntimeError(f"kernel failed: {rc}")
+
+    use_graph = not args.no_graph and kernel == "gemv"
+    graph = None
+    if use_graph:
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            step()  # warm the code objects outside capture
+        torch.cuda.current_stream(dev).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        run = graph.replay
+    else:
+        run = step
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(args.steps):
+        run()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev_s = e0.elapsed_time(e1) / 1e3
+    t = torch.tensor([ev_s], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    launches = args.steps * R
+    flops = 2.0 * M * N * K
+    nbytes = algo_bytes(M, N, K, bits, group, zb)
+    per_launch_s = elapsed / launches
+    value = flops * launches * world / elapsed / 1e12
+    hbm_bound = kernel == "gemv" or M <= 256
+    if hbm_bound:
+        roof = {"bound": "hbm", "achieved": round(nbytes / per_launch_s / 1e9, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    else:
+        roof = {"bound": "mfma", "achieved": round(flops / per_launch_s / 1e12, 2),
+                "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s"}
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    roof["traffic"] = None
+    roof["bytes_per_launch"] = nbytes
+    roof["us_per_launch"] = round(per_launch_s * 1e6, 3)
+    roof["timing"] = ("HIP events over the timed region / launches (graph replay of the ring; "
+                      "includes the inter-kernel dispatch gap)" if use_graph else
+                      "HIP events over the timed region / launches (eager)")
+
+    out = {
+        "metric": "dequant-matmul TFLOP/s + HBM GB/s, int4 g128 4096x4096; LLaMA3-8B PPL delta",
+        "value": round(value, 4),
+        "unit": "TFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": "synthetic",
+        "hbm_GBps_total": round(nbytes * launches * world / elapsed / 1e9, 1),
+        "config": {"workload": args.workload, "note": note, "M": M, "N": N, "K": K,
+                   "bits": bits, "group_size": group, "ring": R, "zero_bits": 8 * zb,
+                   "graph": use_graph, "parallelism": f"weak x{world} (independent rings)"},
+        "roofline": roof,
+        "wall_s": round(wall, 4),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(M, N, K, bits, group, args.cpu_seconds) \
+            if kernel == "gemv" else cpu_baseline(min(M, 32), N, K, bits, group, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/*
+ * qlin_gfx950.h — C ABI of libqlin_gfx950.so, the MI355X (gfx950) quantized-linear hot path.
+ *
+ * Drop-in boundary for SilviaUvA/LLaMA3-Quantization's quantized-linear path.  The reference has no
+ * native code (its arithmetic is PyTorch ops in quant/quantizer.py and F.linear in
+ * quant/int_linear.py); each entry point below replaces the reference interface named in its
+ * comment.  The Python host mirror (llama3-quantization_amd/quant/) binds these through ctypes —
+ * see INTEGRATION.md for the binding a maintainer would add.
+ *
+ * Conventions (all entry points):
+ *   - return 0 on success, otherwise a hipError_t code (1 = hipErrorInvalidValue for bad args);
+ *     no C++ exception crosses the ABI; nothing is printed.
+ *   - the caller owns every buffer (device pointers); the library allocates nothing, never
+ *     synchronises, and enqueues all work on `stream` (a hipStream_t, NULL = legacy default).
+ *   - stateless and reentrant; safe to call from any host thread and inside stream capture.
+ *   - fp16 tensors are passed as uint16_t* (IEEE binary16 bit patterns).
+ *
+ * Canonical packed weight layout ("qlin" layout):
+ *   qweight  uint32 [N, K*bits/32]  K-packed per output row in 32-element lane chunks of `bits`
+ *            words; bits in {2,3,4,8}.  Element order inside a chunk: oracle/quant_oracle.py header.
+ *   scales   fp16   [N, K/group]    == reference scales.view(N, -1)     (quant/omniquant.py:322-325)
+ *   zeros    int8 or int16 [N, K/group] (zero_bits = 8 | 16), integral zero point
+ *            == reference zeros.view(N, -1); disable_zero_point is stored as zero = 2^(bits-1).
+ *   group    multiple of 32 dividing K (group = K for per-channel); K % 32 == 0.
+ */
+#ifndef QLIN_GFX950_H
+#define QLIN_GFX950_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QLIN_ABI_VERSION 1
+
+/* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
+#define QLIN_SYMMETRIC          1
+#define QLIN_DISABLE_ZERO_POINT 2
+#define QLIN_LWC                4
+
+/* element dtypes */
+#define QLIN_F16 0
+#define QLIN_F32 1
+
+/* ABI version (QLIN_ABI_VERSION); lets a binding check it loaded the library it was written for. */
+int qlin_abi_version(void);
+
+/* Human-readable text for a return code. */
+const char* qlin_error_string(int code);
+
+/*
+ * Fused RTN quantizer: per-group min/max calibration + fake-quant (+ optional packing), one pass.
+ * Replaces UniformAffineQuantizer.forward -> per_token_dynamic_calibration -> fake_quant
+ * (quant/quantizer.py:118-159, :94-115), bit-exact in the input dtype (fp16 or fp32).
+ *   x          [rows, K] dtype;  group divides K (group = K: per-channel / per-token).
+ *   lwc_up_sig, lwc_low_sig  [rows*K/group] dtype: sigmoid(upbound/lowbound_factor) (QLIN_LWC).
+ *   x_dq       [rows, K] dtype or NULL;  scale_out / zp_out [rows*K/group] dtype or NULL
+ *              (zp_out unused with QLIN_DISABLE_ZERO_POINT) — the reference's scale /
+ *              round_zero_point tensors.
+ *   qweight, scales, zeros16: canonical packed outputs (dtype must be QLIN_F16), or all NULL;
+ *              zeros are always written as int16 here (narrow to int8 on the host if they fit).
+ */
+int qlin_quantize(const void* x, int dtype, int64_t rows, int64_t K, int bits, int group,
+                  int flags, const void* lwc_up_sig, const void* lwc_low_sig,
+                  void* x_dq, void* scale_out, void* zp_out,
+                  uint32_t* qweight, uint16_t* scales, int16_t* zeros16, void* stream);
+
+/*
+ * fake_quant with given parameters (quant/quantizer.py:94-115): x_dq = RN(RN(clamp(round_ste(
+ * RN(x / s)) + zp) - zp) * s), optionally also packing the integer codes (dtype QLIN_F16 only).
+ *   scale, zp [rows*K/group] dtype (zp NULL iff QLIN_DISABLE_ZERO_POINT); outputs as in
+ *   qlin_quantize; x_dq may be NULL.
+ */
+int qlin_fake_quant(const void* x, int dtype, const void* scale, const void* zp, int64_t rows,
+                    int64_t K, int bits, int group, int flags, void* x_dq, uint32_t* qweight,
+                    uint16_t* scales, int16_t* zeros16, void* stream);
+
+/*
+ * Real-quant packer: canonical layout from (W_dq, scales, zeros) as registered by
+ * register_scales_and_zeros (quant/quantizer.py:161-165).  Replaces the AutoGPTQ
+ * QuantLinear.pack(module, scales, zeros) call of quant/omniquant.py:315-335.  Integer codes are
+ * recovered with the quantizer's own fp16 arithmetic, so qlin_dequant_f16 of the result
+ * reproduces W_dq bit-exactly.
+ *   w_dq [N, K] fp16; scales_ref, zeros_ref [N*K/group] fp16 (zeros_ref NULL iff
+ *   QLIN_DISABLE_ZERO_POINT).  Outputs as in qlin_quantize.
+ */
+int qlin_pack_f16(const uint16_t* w_dq, const uint16_t* scales_ref, const uint16_t* zeros_ref,
+                  int64_t N, int64_t K, int bits, int group, int flags,
+                  uint32_t* qweight, uint16_t* scales, int16_t* zeros16, void* stream);
+
+/*
+ * Dequantize the canonical layout: w[n,k] = RN16(RN16(q - zp) * s), bit-exact with the reference
+ * fake_quant's x_dequant.sub(zp).mul(scale) (quant/quantizer.py:107-110).  Debug / parity and
+ * the fake-quant eval mode (module.weight = W_dq, quant/utils.py:133-136).
+ */
+int qlin_dequant_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
+                     int zero_bits, int64_t N, int64_t K, int bits, int group, uint16_t* w,
+                     void* stream);
+
+/*
+ * y[M, N] = x[M, K] @ W_dq[N, K]^T (+ bias[N]) with the group-wise unpack + dequant fused into the
+ * product; fp16 in/out, fp32 accumulation.  Replaces QuantLinear.forward's
+ * fwd_func(input, weight, bias) = F.linear (quant/int_linear.py:62) on packed weights.
+ *   qlin_gemv_f16: wave64 GEMV, 1 <= M <= 4 (decode).
+ *   qlin_gemm_f16: MFMA (v_mfma_f32_*_f16) tiles, any M >= 1 (prefill / PPL windows).
+ *   qlin_linear_f16: picks one of the two from M.
+ *   workspace: reserved, pass NULL.
+ */
+int qlin_gemv_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
+                  int zero_bits, const uint16_t* x, const uint16_t* bias, uint16_t* y,
+                  int64_t M, int64_t N, int64_t K, int bits, int group, void* stream);
+int qlin_gemm_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
+                  int zero_bits, const uint16_t* x, const uint16_t* bias, uint16_t* y,
+                  int64_t M, int64_t N, int64_t K, int bits, int group, void* workspace,
+                  void* stream);
+int qlin_linear_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
+                    int zero_bits, const uint16_t* x, const uint16_t* bias, uint16_t* y,
+                    int64_t M, int64_t N, int64_t K, int bits, int group, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QLIN_GFX950_H */

@@ -1,0 +1,361 @@
+// qlin_quantize.hip — fused RTN quantizer (calibrate + fake-quant + pack) and the real-quant
+// packer, gfx950.
+//
+// Replaces UniformAffineQuantizer.forward (quant/quantizer.py:118-130): per-group amin/amax
+// (:141-142), optional LWC clipping (:143-145), symmetric / asymmetric scale and zero point
+// (:146-159), then fake_quant (:94-115) — every op rounded to the element dtype exactly as the
+// reference's fp16/fp32 torch ops round (oracle/quant_oracle.py restates the same arithmetic).
+//
+// Work decomposition: a block of 256 threads owns RPB whole rows; a thread owns 32-element lane
+// chunks (the packing granule).  Phase 1 reduces each chunk's min/max into LDS; phase 2 reduces
+// one group per thread (a group never crosses a row) and computes (scale, zp); phase 3 re-reads
+// the chunk (L2-hot), fake-quantizes it and writes x_dq and/or the packed words.
+#include "qlin_common.h"
+#include "../../include/qlin_gfx950.h"
+
+using namespace qlin;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxChunks = 1024;  // chunks per block: K <= 32768
+
+struct QP {
+  int64_t rows;
+  int K, group, cpr, cpg, rpb, bits, flags;
+  float qmin, qmax;
+};
+
+template <typename T>
+__device__ __forceinline__ void load32(const T* __restrict__ p, float (&v)[32]) {
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const h8 h = *reinterpret_cast<const h8*>(p + 8 * i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[8 * i + j] = (float)h[j];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float4 f = *reinterpret_cast<const float4*>(p + 4 * i);
+      v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store32(T* __restrict__ p, const float (&v)[32]) {
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      h8 h;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[8 * i + j];
+      *reinterpret_cast<h8*>(p + 8 * i) = h;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      *reinterpret_cast<float4*>(p + 4 * i) = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+  }
+}
+
+// pack 32 unsigned codes (as floats holding exact small integers) into BITS words
+template <int BITS>
+__device__ __forceinline__ void pack_chunk(const uint32_t (&u)[32], uint32_t* __restrict__ out) {
+  if constexpr (BITS == 2 || BITS == 4 || BITS == 8) {
+    constexpr int P = 16 / BITS;
+#pragma unroll
+    for (int i = 0; i < BITS; ++i) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        w |= u[i * 2 * P + 2 * p] << (BITS * p);
+        w |= u[i * 2 * P + 2 * p + 1] << (16 + BITS * p);
+      }
+      out[i] = w;
+    }
+  } else {  // 3: low two bits in the 2-bit layout, bit 2 in word 2
+    uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      w0 |= (u[2 * p] & 3u) << (2 * p);
+      w0 |= (u[2 * p + 1] & 3u) << (16 + 2 * p);
+      w1 |= (u[16 + 2 * p] & 3u) << (2 * p);
+      w1 |= (u[16 + 2 * p + 1] & 3u) << (16 + 2 * p);
+    }
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      w2 |= ((u[2 * p] >> 2) & 1u) << p;
+      w2 |= ((u[2 * p + 1] >> 2) & 1u) << (16 + p);
+    }
+    out[0] = w0; out[1] = w1; out[2] = w2;
+  }
+}
+
+// (scale, zp) of one group — quant/quantizer.py:141-159
+template <typename T>
+__device__ __forceinline__ void calib(float xmin, float xmax, float up, float low, const QP& P,
+                                      float& scale, float& zp) {
+#pragma clang fp contract(off)
+  using E = Elt<T>;
+  if (P.flags & QLIN_LWC) {
+    xmax = E::rn(up * xmax);
+    xmin = E::rn(low * xmin);
+  }
+  if (P.flags & QLIN_SYMMETRIC) {
+    const float am = max_nan(fabsf(xmax), fabsf(xmin));
+    scale = E::rn(am / (float)((1 << (P.bits - 1)) - 1));
+    scale = E::rn(clamp_nan(scale, 1e-5f, 1e4f));
+    zp = (float)((1 << (P.bits - 1)) - 1);
+  } else {
+    const float range = E::rn(xmax - xmin);
+    scale = E::rn(range / (float)((1 << P.bits) - 1));
+    scale = E::rn(clamp_nan(scale, 1e-5f, 1e4f));
+    zp = E::rn(-xmin / scale);
+  }
+  zp = rintf(E::rn(clamp_nan(zp, -1e4f, 1e4f)));
+}
+
+// fake_quant of one element — quant/quantizer.py:103-110 (round_ste forward = (r - v) + v)
+template <typename T>
+__device__ __forceinline__ float fq(float x, float s, float zp, bool has_zp, const QP& P,
+                                    float& xi_out) {
+#pragma clang fp contract(off)
+  using E = Elt<T>;
+  const float v = E::rn(x / s);
+  const float r = rintf(v);
+  float xi = E::rn(E::rn(r - v) + v);
+  if (has_zp) xi = E::rn(xi + zp);
+  xi = clamp_nan(xi, P.qmin, P.qmax);
+  xi_out = xi;
+  float d = xi;
+  if (has_zp) d = E::rn(d - zp);
+  return E::rn(d * s);
+}
+
+template <typename T, int BITS>  // BITS == 0: no packed output
+__global__ __launch_bounds__(kThreads) void quantize_kernel(
+    const T* __restrict__ x, QP P, const T* __restrict__ up, const T* __restrict__ low,
+    T* __restrict__ x_dq, T* __restrict__ scale_out, T* __restrict__ zp_out,
+    uint32_t* __restrict__ qweight, _Float16* __restrict__ scales, int16_t* __restrict__ zeros16) {
+  __shared__ float s_min[kMaxChunks];
+  __shared__ float s_max[kMaxChunks];
+  __shared__ float s_scale[kMaxChunks];
+  __shared__ float s_zp[kMaxChunks];
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * P.rpb;
+  const int nrows = (int)min((int64_t)P.rpb, P.rows - row0);
+  const int nch = nrows * P.cpr;
+  const bool has_zp = !(P.flags & QLIN_DISABLE_ZERO_POINT);
+  const T* xb = x + row0 * P.K;
+
+  // phase 1: chunk min / max
+  for (int c = tid; c < nch; c += kThreads) {
+    float v[32];
+    load32<T>(xb + (int64_t)c * 32, v);
+    float mn = v[0], mx = v[0];
+#pragma unroll
+    for (int i = 1; i < 32; ++i) { mn = min_nan(mn, v[i]); mx = max_nan(mx, v[i]); }
+    s_min[c] = mn;
+    s_max[c] = mx;
+  }
+  __syncthreads();
+
+  // phase 2: one group per thread
+  const int ngr = nch / P.cpg;
+  const int64_t g0 = row0 * (P.K / P.group);
+  for (int gi = tid; gi < ngr; gi += kThreads) {
+    float mn = s_min[gi * P.cpg], mx = s_max[gi * P.cpg];
+    for (int j = 1; j < P.cpg; ++j) {
+      mn = min_nan(mn, s_min[gi * P.cpg + j]);
+      mx = max_nan(mx, s_max[gi * P.cpg + j]);
+    }
+    float upf = 1.f, lowf = 1.f;
+    if (P.flags & QLIN_LWC) { upf = (float)up[g0 + gi]; lowf = (float)low[g0 + gi]; }
+    float scale, zp;
+    calib<T>(mn, mx, upf, lowf, P, scale, zp);
+    s_scale[gi] = scale;
+    s_zp[gi] = zp;
+    if (scale_out) scale_out[g0 + gi] = (T)scale;
+    if (zp_out && has_zp) zp_out[g0 + gi] = (T)zp;
+    if constexpr (BITS > 0) {
+      scales[g0 + gi] = (_Float16)scale;
+      zeros16[g0 + gi] = has_zp ? (int16_t)zp : (int16_t)(1 << (BITS - 1));
+    }
+  }
+  __syncthreads();
+
+  // phase 3: fake-quant (+ pack)
+  for (int c = tid; c < nch; c += kThreads) {
+    float v[32];
+    load32<T>(xb + (int64_t)c * 32, v);
+    const int gi = c / P.cpg;
+    const float s = s_scale[gi], zp = s_zp[gi];
+    float o[32];
+    uint32_t u[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      float xi;
+      o[i] = fq<T>(v[i], s, zp, has_zp, P, xi);
+      if (!has_zp) xi += (float)(1 << (P.bits - 1));
+      u[i] = (xi == xi) ? (uint32_t)(int)xi : 0u;  // NaN (x/s overflow) has no code: 0
+    }
+    if (x_dq) store32<T>(x_dq + row0 * P.K + (int64_t)c * 32, o);
+    if constexpr (BITS > 0) {
+      const int r = c / P.cpr, cc = c - r * P.cpr;
+      pack_chunk<BITS>(u, qweight + (row0 + r) * (int64_t)(P.cpr * BITS) + (int64_t)cc * BITS);
+    }
+  }
+}
+
+// fake_quant with given (scale, zp) — quant/quantizer.py:94-115 — optionally packing the codes.
+// Applied to W_dq with its registered (scales, zeros) it is the real-quant packer
+// (quant/omniquant.py:315-335): the codes are recovered with the quantizer's own arithmetic.
+template <typename T, int BITS>  // BITS == 0: no packed output
+__global__ __launch_bounds__(kThreads) void fq_kernel(
+    const T* __restrict__ x, const T* __restrict__ sref, const T* __restrict__ zref,
+    int64_t total_chunks, int K, int group, int bits, int flags, T* __restrict__ x_dq,
+    uint32_t* __restrict__ qweight, _Float16* __restrict__ scales, int16_t* __restrict__ zeros16) {
+  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (c >= total_chunks) return;
+  const int cpr = K / 32;
+  const int64_t row = c / cpr;
+  const int cc = (int)(c - row * cpr);
+  const int64_t gidx = row * (K / group) + (int64_t)cc * 32 / group;
+  const bool has_zp = !(flags & QLIN_DISABLE_ZERO_POINT);
+  QP P;
+  P.bits = bits;
+  P.qmin = has_zp ? 0.f : -(float)(1 << (bits - 1));
+  P.qmax = has_zp ? (float)((1 << bits) - 1) : (float)((1 << (bits - 1)) - 1);
+  const float s = (float)sref[gidx];
+  const float zp = has_zp ? (float)zref[gidx] : 0.f;
+  float v[32];
+  load32<T>(x + c * 32, v);
+  float o[32];
+  uint32_t u[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    float xi;
+    o[i] = fq<T>(v[i], s, zp, has_zp, P, xi);
+    if (!has_zp) xi += (float)(1 << (bits - 1));
+    u[i] = (xi == xi) ? (uint32_t)(int)xi : 0u;
+  }
+  if (x_dq) store32<T>(x_dq + c * 32, o);
+  if constexpr (BITS > 0) {
+    pack_chunk<BITS>(u, qweight + c * BITS);
+    if ((cc * 32) % group == 0) {
+      scales[gidx] = (_Float16)s;
+      zeros16[gidx] = has_zp ? (int16_t)zp : (int16_t)(1 << (BITS - 1));
+    }
+  }
+}
+
+template <typename T>
+int launch_quantize(const void* x, int64_t rows, int64_t K, int bits, int group, int flags,
+                    const void* up, const void* low, void* x_dq, void* scale_out, void* zp_out,
+                    uint32_t* qweight, uint16_t* scales, int16_t* zeros16, hipStream_t st) {
+  QP P;
+  P.rows = rows;
+  P.K = (int)K;
+  P.group = group;
+  P.cpr = (int)(K / 32);
+  P.cpg = group / 32;
+  P.rpb = P.cpr >= kThreads ? 1 : kThreads / P.cpr;
+  P.bits = bits;
+  P.flags = flags;
+  const bool has_zp = !(flags & QLIN_DISABLE_ZERO_POINT);
+  P.qmin = has_zp ? 0.f : -(float)(1 << (bits - 1));
+  P.qmax = has_zp ? (float)((1 << bits) - 1) : (float)((1 << (bits - 1)) - 1);
+  const dim3 grid((unsigned)((rows + P.rpb - 1) / P.rpb));
+  const bool pack = qweight != nullptr;
+  const T* xx = (const T*)x;
+#define QLIN_Q(B)                                                                            \
+  hipLaunchKernelGGL((quantize_kernel<T, B>), grid, dim3(kThreads), 0, st, xx, P,            \
+                     (const T*)up, (const T*)low, (T*)x_dq, (T*)scale_out, (T*)zp_out,       \
+                     qweight, (_Float16*)scales, zeros16)
+  if (!pack) QLIN_Q(0);
+  else if (bits == 2) QLIN_Q(2);
+  else if (bits == 3) QLIN_Q(3);
+  else if (bits == 4) QLIN_Q(4);
+  else QLIN_Q(8);
+#undef QLIN_Q
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int qlin_abi_version(void) { return QLIN_ABI_VERSION; }
+
+extern "C" const char* qlin_error_string(int code) {
+  if (code == QLIN_OK) return "ok";
+  if (code == QLIN_EINVAL) return "invalid argument";
+  return hipGetErrorString((hipError_t)code);
+}
+
+extern "C" int qlin_quantize(const void* x, int dtype, int64_t rows, int64_t K, int bits,
+                             int group, int flags, const void* lwc_up_sig,
+                             const void* lwc_low_sig, void* x_dq, void* scale_out, void* zp_out,
+                             uint32_t* qweight, uint16_t* scales, int16_t* zeros16,
+                             void* stream) {
+  if (!x || rows < 0 || K <= 0 || K % 32 || K / 32 > kMaxChunks || group <= 0 || group % 32 ||
+      K % group || bits < 2 || bits > 8 || (dtype != QLIN_F16 && dtype != QLIN_F32))
+    return QLIN_EINVAL;
+  if ((flags & QLIN_LWC) && (!lwc_up_sig || !lwc_low_sig)) return QLIN_EINVAL;
+  const bool pack = qweight || scales || zeros16;
+  if (pack && (!qweight || !scales || !zeros16 || dtype != QLIN_F16 ||
+               !(bits == 2 || bits == 3 || bits == 4 || bits == 8)))
+    return QLIN_EINVAL;
+  if (rows == 0) return QLIN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == QLIN_F16)
+    return launch_quantize<_Float16>(x, rows, K, bits, group, flags, lwc_up_sig, lwc_low_sig,
+                                     x_dq, scale_out, zp_out, qweight, scales, zeros16, st);
+  return launch_quantize<float>(x, rows, K, bits, group, flags, lwc_up_sig, lwc_low_sig, x_dq,
+                                scale_out, zp_out, nullptr, nullptr, nullptr, st);
+}
+
+extern "C" int qlin_fake_quant(const void* x, int dtype, const void* scale, const void* zp,
+                               int64_t rows, int64_t K, int bits, int group, int flags,
+                               void* x_dq, uint32_t* qweight, uint16_t* scales, int16_t* zeros16,
+                               void* stream) {
+  const bool has_zp = !(flags & QLIN_DISABLE_ZERO_POINT);
+  const bool pack = qweight || scales || zeros16;
+  if (!x || !scale || (has_zp && !zp) || rows < 0 || K <= 0 || K % 32 || group <= 0 ||
+      group % 32 || K % group || bits < 2 || bits > 8 || (dtype != QLIN_F16 && dtype != QLIN_F32))
+    return QLIN_EINVAL;
+  if (pack && (!qweight || !scales || !zeros16 || dtype != QLIN_F16 ||
+               !(bits == 2 || bits == 3 || bits == 4 || bits == 8)))
+    return QLIN_EINVAL;
+  const int64_t chunks = rows * (K / 32);
+  if (chunks == 0) return QLIN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)((chunks + kThreads - 1) / kThreads));
+  if (dtype == QLIN_F32) {
+    hipLaunchKernelGGL((fq_kernel<float, 0>), grid, dim3(kThreads), 0, st, (const float*)x,
+                       (const float*)scale, (const float*)zp, chunks, (int)K, group, bits, flags,
+                       (float*)x_dq, nullptr, nullptr, nullptr);
+    return (int)hipGetLastError();
+  }
+#define QLIN_P(B)                                                                            \
+  hipLaunchKernelGGL((fq_kernel<_Float16, B>), grid, dim3(kThreads), 0, st, (const _Float16*)x, \
+                     (const _Float16*)scale, (const _Float16*)zp, chunks, (int)K, group, bits,  \
+                     flags, (_Float16*)x_dq, qweight, (_Float16*)scales, zeros16)
+  if (!pack) QLIN_P(0);
+  else if (bits == 2) QLIN_P(2);
+  else if (bits == 3) QLIN_P(3);
+  else if (bits == 4) QLIN_P(4);
+  else QLIN_P(8);
+#undef QLIN_P
+  return (int)hipGetLastError();
+}
+
+extern "C" int qlin_pack_f16(const uint16_t* w_dq, const uint16_t* scales_ref,
+                             const uint16_t* zeros_ref, int64_t N, int64_t K, int bits, int group,
+                             int flags, uint32_t* qweight, uint16_t* scales, int16_t* zeros16,
+                             void* stream) {
+  if (!w_dq || !qweight || !scales || !zeros16) return QLIN_EINVAL;
+  return qlin_fake_quant(w_dq, QLIN_F16, scales_ref, zeros_ref, N, K, bits, group, flags, nullptr,
+                         qweight, scales, zeros16, stream);
+}

@@ -1,0 +1,264 @@
+"""QuantLlamaDecoderLayer — per-layer dispatch of the reference (models/int_llama_layer.py:20-368).
+
+7 QuantLinear (q/k/v/o, gate/up/down) + 2 QuantMatMul (QK^T, PV) + 2 RMSNorm per layer, same
+constructor signature ``(config, ori_layer, args)`` and forward signature as the reference.
+
+RoPE follows the transformers-4.37.2 contract the reference was written against
+(``rotary_emb(x, seq_len)`` -> cos/sin cache in x.dtype; ``apply_rotary_pos_emb(q, k, cos, sin,
+position_ids)``), restated here because the installed transformers no longer has it.
+
+Dtype policy (documented deviation): the reference casts q to fp32 (:117) but not
+k/v, so its fp16 path raises in QK^T; here k and v are promoted to q's dtype for the two
+attention matmuls (fp32 attention core, as the reference intends), and the attention output is
+cast back to the layer's activation dtype before o_proj.  In fp32 this is exactly the reference.
+"""
+import math
+from typing import Optional, Tuple
+
+import torch
+from torch import nn
+
+from quant.int_linear import QuantLinear
+from quant.int_matmul import QuantMatMul
+from quant.omni_norm import OmniLlamaRMSNorm
+
+
+def _rope_theta(config):
+    if getattr(config, "rope_theta", None) is not None:
+        return float(config.rope_theta)
+    rp = getattr(config, "rope_parameters", None) or {}
+    return float(rp.get("rope_theta", 10000.0))
+
+
+class LlamaRotaryEmbedding437(nn.Module):
+    """cos/sin cache with the transformers-4.37.2 LlamaRotaryEmbedding semantics."""
+
+    def __init__(self, dim, max_position_embeddings=2048, base=10000, device=None):
+        super().__init__()
+        self.dim = dim
+        self.max_position_embeddings = max_position_embeddings
+        self.base = base
+        inv_freq = 1.0 / (self.base ** (torch.arange(0, self.dim, 2, device=device).float() / self.dim))
+        self.register_buffer("inv_freq", inv_freq, persistent=False)
+        self._set_cos_sin_cache(max_position_embeddings, device)
+
+    def _set_cos_sin_cache(self, seq_len, device):
+        self.max_seq_len_cached = seq_len
+        t = torch.arange(seq_len, device=device, dtype=self.inv_freq.dtype)
+        freqs = torch.outer(t, self.inv_freq.to(t.device))
+        emb = torch.cat((freqs, freqs), dim=-1)
+        self.register_buffer("cos_cached", emb.cos(), persistent=False)
+        self.register_buffer("sin_cached", emb.sin(), persistent=False)
+
+    def forward(self, x, seq_len=None):
+        if seq_len > self.max_seq_len_cached:
+            self._set_cos_sin_cache(seq_len, x.device)
+        return (self.cos_cached[:seq_len].to(device=x.device, dtype=x.dtype),
+                self.sin_cached[:seq_len].to(device=x.device, dtype=x.dtype))
+
+
+def rotate_half(x):
+    x1 = x[..., : x.shape[-1] // 2]
+    x2 = x[..., x.shape[-1] // 2:]
+    return torch.cat((-x2, x1), dim=-1)
+
+
+def apply_rotary_pos_emb(q, k, cos, sin, position_ids, unsqueeze_dim=1):
+    cos = cos[position_ids].unsqueeze(unsqueeze_dim)
+    sin = sin[position_ids].unsqueeze(unsqueeze_dim)
+    return (q * cos) + (rotate_half(q) * sin), (k * cos) + (rotate_half(k) * sin)
+
+
+def repeat_kv(hidden_states: torch.Tensor, n_rep: int) -> torch.Tensor:
+    b, h, s, d = hidden_states.shape
+    if n_rep == 1:
+        return hidden_states
+    hidden_states = hidden_states[:, :, None, :, :].expand(b, h, n_rep, s, d)
+    return hidden_states.reshape(b, h * n_rep, s, d)
+
+
+def _act(name):
+    if name == "silu":
+        return nn.functional.silu
+    if name == "relu":
+        return nn.functional.relu
+    if name in ("gelu", "gelu_new", "gelu_pytorch_tanh"):
+        return (lambda x: nn.functional.gelu(x, approximate="tanh")) if name != "gelu" else nn.functional.gelu
+    raise ValueError(f"unsupported hidden_act {name}")
+
+
+class QuantLlamaMLP(nn.Module):
+    def __init__(self, org_module: nn.Module, hidden_size: int, intermediate_size: int,
+                 hidden_act: str, args=None):
+        super().__init__()
+        self.gate_proj = QuantLinear(org_module.gate_proj, args.weight_quant_params, args.act_quant_params)
+        self.down_proj = QuantLinear(org_module.down_proj, args.weight_quant_params, args.act_quant_params)
+        self.up_proj = QuantLinear(org_module.up_proj, args.weight_quant_params, args.act_quant_params)
+        self.act_fn = _act(hidden_act)
+
+    def forward(self, x):
+        return self.down_proj(self.act_fn(self.gate_proj(x)) * self.up_proj(x))
+
+
+class QuantLlamaAttention(nn.Module):
+    """Multi-headed attention from 'Attention Is All You Need' paper"""
+
+    def __init__(self, org_module: nn.Module, config, args=None):
+        super().__init__()
+        self.config = config
+        self.hidden_size = config.hidden_size
+        self.num_heads = config.num_attention_heads
+        self.head_dim = self.hidden_size // self.num_heads
+        self.num_key_value_heads = config.num_key_value_heads
+        self.num_key_value_groups = self.num_heads // self.num_key_value_heads
+        self.max_position_embeddings = config.max_position_embeddings
+        if (self.head_dim * self.num_heads) != self.hidden_size:
+            raise ValueError(
+                f"hidden_size must be divisible by num_heads (got `hidden_size`: {self.hidden_size}"
+                f" and `num_heads`: {self.num_heads}).")
+        rot = getattr(org_module, "rotary_emb", None)
+        if rot is not None and hasattr(rot, "cos_cached"):
+            self.rotary_emb = rot
+        else:
+            self.rotary_emb = LlamaRotaryEmbedding437(
+                self.head_dim, self.max_position_embeddings, _rope_theta(config),
+                device=org_module.q_proj.weight.device)
+        self.k_proj = QuantLinear(org_module.k_proj, args.weight_quant_params, args.act_quant_params)
+        self.v_proj = QuantLinear(org_module.v_proj, args.weight_quant_params, args.act_quant_params)
+        self.q_proj = QuantLinear(org_module.q_proj, args.weight_quant_params, args.act_quant_params)
+        self.o_proj = QuantLinear(org_module.o_proj, args.weight_quant_params, args.act_quant_params)
+        self.qkt_matmul = QuantMatMul(args.q_quant_params, args.k_quant_params, matmul_func=torch.matmul)
+        self.pv_matmul = QuantMatMul(args.p_quant_params, args.v_quant_params, matmul_func=torch.matmul)
+        self.use_weight_quant = False
+        self.use_act_quant = False
+
+    def _shape(self, tensor: torch.Tensor, seq_len: int, bsz: int):
+        return tensor.view(bsz, seq_len, self.num_heads, self.head_dim).transpose(1, 2).contiguous()
+
+    def forward(
+        self,
+        hidden_states: torch.Tensor,
+        attention_mask: Optional[torch.Tensor] = None,
+        position_ids: Optional[torch.LongTensor] = None,
+        past_key_value: Optional[Tuple[torch.Tensor]] = None,
+        output_attentions: bool = False,
+        use_cache: bool = False,
+    ):
+        bsz, q_len, _ = hidden_states.size()
+        act_dtype = hidden_states.dtype
+        query_states = self.q_proj(hidden_states).view(bsz, q_len, self.num_heads, self.head_dim).transpose(1, 2).type(torch.float32)
+        key_states = self.k_proj(hidden_states).view(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
+        value_states = self.v_proj(hidden_states).view(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
+
+        kv_seq_len = key_states.shape[-2]
+        if past_key_value is not None:
+            kv_seq_len += past_key_value[0].shape[-2]
+        if position_ids is None:
+            position_ids = torch.arange(kv_seq_len - q_len, kv_seq_len, device=hidden_states.device)[None]
+        cos, sin = self.rotary_emb(value_states, seq_len=kv_seq_len)
+        query_states, key_states = apply_rotary_pos_emb(query_states, key_states, cos, sin, position_ids)
+
+        if past_key_value is not None:
+            key_states = torch.cat([past_key_value[0], key_states], dim=2)
+            value_states = torch.cat([past_key_value[1], value_states], dim=2)
+        past_key_value = (key_states, value_states) if use_cache else None
+
+        key_states = repeat_kv(key_states, self.num_key_value_groups)
+        value_states = repeat_kv(value_states, self.num_key_value_groups)
+
+        query_states = self.qkt_matmul.quant_x1(query_states)
+        key_states = self.qkt_matmul.quant_x2(key_states)
+        attn_weights = self.qkt_matmul(query_states, key_states.to(query_states.dtype).transpose(2, 3)) / math.sqrt(self.head_dim)
+
+        if attn_weights.size() != (bsz, self.num_heads, q_len, kv_seq_len):
+            raise ValueError(
+                f"Attention weights should be of size {(bsz, self.num_heads, q_len, kv_seq_len)}, but is"
+                f" {attn_weights.size()}")
+        if attention_mask is not None:
+            if attention_mask.size() != (bsz, 1, q_len, kv_seq_len):
+                raise ValueError(
+                    f"Attention mask should be of size {(bsz, 1, q_len, kv_seq_len)}, but is {attention_mask.size()}")
+            attn_weights = attn_weights + attention_mask
+            attn_weights = torch.max(attn_weights, torch.tensor(torch.finfo(attn_weights.dtype).min, device=attn_weights.device))
+
+        attn_weights = nn.functional.softmax(attn_weights, dim=-1, dtype=torch.float32).to(query_states.dtype)
+        attn_weights = self.pv_matmul.quant_x1(attn_weights)
+        value_states = self.pv_matmul.quant_x2(value_states)
+        attn_output = self.pv_matmul(attn_weights, value_states.to(attn_weights.dtype))
+
+        if attn_output.size() != (bsz, self.num_heads, q_len, self.head_dim):
+            raise ValueError(
+                f"`attn_output` should be of size {(bsz, self.num_heads, q_len, self.head_dim)}, but is"
+                f" {attn_output.size()}")
+        attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
+        attn_output = self.o_proj(attn_output)
+        if not output_attentions:
+            attn_weights = None
+        return attn_output, attn_weights, past_key_value
+
+    def set_quant_state(self, weight_quant: bool = False, act_quant: bool = False):
+        self.use_weight_quant = weight_quant
+        self.use_act_quant = act_quant
+        for m in self.modules():
+            if isinstance(m, (QuantLinear, QuantMatMul)):
+                m.set_quant_state(weight_quant, act_quant)
+
+
+class QuantLlamaDecoderLayer(nn.Module):
+    def __init__(self, config, ori_layer, args):
+        super().__init__()
+        self.hidden_size = config.hidden_size
+        self.self_attn = QuantLlamaAttention(org_module=ori_layer.self_attn, config=config, args=args)
+        self.mlp = QuantLlamaMLP(org_module=ori_layer.mlp, hidden_size=self.hidden_size,
+                                 intermediate_size=config.intermediate_size,
+                                 hidden_act=config.hidden_act, args=args)
+        self.input_layernorm = OmniLlamaRMSNorm(ori_layer.input_layernorm, eps=ori_layer.input_layernorm.variance_epsilon)
+        self.post_attention_layernorm = OmniLlamaRMSNorm(ori_layer.post_attention_layernorm, eps=ori_layer.post_attention_layernorm.variance_epsilon)
+        self.let = False
+
+    def forward(
+        self,
+        hidden_states: torch.Tensor,
+        attention_mask: Optional[torch.Tensor] = None,
+        position_ids: Optional[torch.LongTensor] = None,
+        past_key_value: Optional[Tuple[torch.Tensor]] = None,
+        output_attentions: Optional[bool] = False,
+        use_cache: Optional[bool] = False,
+    ):
+        residual = hidden_states
+        hidden_states = self.input_layernorm(hidden_states)
+        hidden_states, self_attn_weights, present_key_value = self.self_attn(
+            hidden_states=hidden_states, attention_mask=attention_mask, position_ids=position_ids,
+            past_key_value=past_key_value, output_attentions=output_attentions, use_cache=use_cache)
+        hidden_states = residual + hidden_states
+        residual = hidden_states
+        hidden_states = self.post_attention_layernorm(hidden_states)
+        hidden_states = self.mlp(hidden_states)
+        hidden_states = residual + hidden_states
+        outputs = (hidden_states,)
+        if output_attentions:
+            outputs += (self_attn_weights,)
+        if use_cache:
+            outputs += (present_key_value,)
+        return outputs
+
+    def set_quant_state(self, weight_quant: bool = False, act_quant: bool = False):
+        self.use_weight_quant = weight_quant
+        self.use_act_quant = act_quant
+        for name, m in self.named_modules():
+            if isinstance(m, (QuantLinear, QuantMatMul)):
+                m.set_quant_state(weight_quant, act_quant)
+
+    @torch.no_grad()
+    def smooth_and_quant_inplace(self):
+        if self.let:
+            raise NotImplementedError("LET smoothing is out of scope for the MI355X hot path")
+        for name, module in self.named_modules():
+            if isinstance(module, QuantLinear):
+                module.weight = module.weight_quantizer(module.weight)
+                module.use_temporary_parameter = False
+
+    def register_scales_and_zeros(self):
+        for name, module in self.named_modules():
+            if isinstance(module, QuantLinear):
+                module.weight_quantizer.register_scales_and_zeros()

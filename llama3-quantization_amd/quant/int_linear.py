@@ -1,0 +1,162 @@
+"""QuantLinear — MI355X build of the reference drop-in nn.Linear (quant/int_linear.py:11-69).
+
+Reference behaviour is kept verbatim at the module level:
+  * constructor ``QuantLinear(org_module, weight_quant_params, act_quant_params,
+    disable_input_quant)``; ``weight``/``bias`` buffers share storage with ``org_module``;
+  * ``forward`` picks temp_weight / weight_quantizer(weight) / weight, optionally fake-quantizes the
+    input per token, then calls ``self.fwd_func(input, weight, bias, **self.fwd_kwargs)``;
+  * ``set_quant_state(weight_quant, act_quant)``.
+
+Added (the real-quant path of quant/omniquant.py:315-335, re-done for MI355X):
+  * ``pack()`` — after ``register_scales_and_zeros`` (weight == W_dq), packs the codes into the
+    canonical gfx950 layout (``qlin_pack_f16``) and switches ``fwd_func`` to the fused
+    unpack + dequant + GEMV/MFMA-GEMM kernels (``qlin_linear_f16``).  ``pack_from_weight()`` does the
+    RTN quantize + pack of a float weight in one kernel.
+  * ``packed`` / ``qweight`` / ``qscales`` / ``qzeros`` / ``wbits`` / ``group`` state.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import qlin
+from .quantizer import UniformAffineQuantizer
+
+
+class QuantLinear(nn.Module):
+    """
+    Quantized Module that can perform quantized convolution or normal convolution.
+    To activate quantization, please use set_quant_state function.
+    """
+
+    def __init__(
+        self,
+        org_module: nn.Linear,
+        weight_quant_params: dict = {},
+        act_quant_params: dict = {},
+        disable_input_quant=False,
+    ):
+        super().__init__()
+        self.fwd_kwargs = dict()
+        self.fwd_func = F.linear
+        self.register_buffer("weight", org_module.weight)
+        if org_module.bias is not None:
+            self.register_buffer("bias", org_module.bias)
+        else:
+            self.bias = None
+        self.in_features = org_module.in_features
+        self.out_features = org_module.out_features
+        self.use_weight_quant = False
+        self.use_act_quant = False
+        self.weight_quantizer = UniformAffineQuantizer(**weight_quant_params,
+                                                       shape=org_module.weight.shape)
+        if not disable_input_quant:
+            self.act_quantizer = UniformAffineQuantizer(**act_quant_params)
+        else:
+            self.act_quantizer = None
+        self.disable_input_quant = disable_input_quant
+        self.use_temporary_parameter = False
+        self.packed = False
+        self.wbits = None
+        self.group = None
+
+    def forward(self, input: torch.Tensor):
+        if self.packed:
+            weight = None
+            bias = self.bias
+        elif self.use_temporary_parameter:
+            weight = self.temp_weight
+            bias = self.temp_bias
+        elif self.use_weight_quant:
+            weight = self.weight_quantizer(self.weight)
+            bias = self.bias
+        else:
+            weight = self.weight
+            bias = self.bias
+
+        if self.use_act_quant and not self.disable_input_quant:
+            input = self.act_quantizer(input)
+
+        out = self.fwd_func(input, weight, bias, **self.fwd_kwargs)
+        return out
+
+    def set_quant_state(self, weight_quant: bool = False, act_quant: bool = False):
+        self.use_weight_quant = weight_quant
+        self.use_act_quant = act_quant
+
+    # ------------------------------------------------------------------------------------------
+    # packed (real-quant) mode
+    # ------------------------------------------------------------------------------------------
+    def _packed_fwd(self, input, weight, bias):
+        x = input
+        if x.dtype != torch.float16:
+            x = x.to(torch.float16)
+        y = qlin.linear(x.contiguous(), self.qweight, self.qscales, self.qzeros,
+                        None if bias is None else bias.to(torch.float16).contiguous(),
+                        self.out_features, self.in_features, self.wbits, self.group)
+        return y if input.dtype == torch.float16 else y.to(input.dtype)
+
+    def _install(self, qweight, scales, zeros, bits, group, keep_weight):
+        self.register_buffer("qweight", qweight)
+        self.register_buffer("qscales", scales)
+        self.register_buffer("qzeros", qlin.narrow_zeros(zeros))
+        self.wbits = bits
+        self.group = group
+        self.packed = True
+        self.fwd_func = self._packed_fwd
+        self.fwd_kwargs = {}
+        if not keep_weight:
+            self.weight = None
+
+    def _check_packable(self):
+        wq = self.weight_quantizer
+        if not self.weight.is_cuda:
+            raise RuntimeError("pack() runs the gfx950 packer: move the module to the GPU first")
+        if wq.n_bits not in (2, 3, 4, 8):
+            raise ValueError(f"packed mode supports 2/3/4/8-bit weights, not {wq.n_bits}")
+        if wq.deficiency:
+            raise ValueError("packed mode needs in_features % group_size == 0")
+        return wq.group_size or self.in_features
+
+    @torch.no_grad()
+    def pack(self, keep_weight=False):
+        """Pack W_dq with the registered (scales, zeros) — the reference's ``--real_quant`` step
+        (quant/omniquant.py:315-335) with the gfx950 layout in place of AutoGPTQ's."""
+        wq = self.weight_quantizer
+        group = self._check_packable()
+        if not hasattr(wq, "scales"):
+            raise RuntimeError("call register_scales_and_zeros() before pack()")
+        w = self.weight.to(torch.float16).contiguous()
+        s = wq.scales.to(torch.float16).reshape(-1).contiguous()
+        z = None if wq.zeros is None else wq.zeros.to(torch.float16).reshape(-1).contiguous()
+        flags = qlin.DISABLE_ZERO_POINT if z is None else 0
+        out = qlin.fake_quant(w, s, z, wq.n_bits, group, flags, want_xdq=False, pack=True)
+        self._install(out["qweight"], out["scales"], out["zeros"], wq.n_bits, group, keep_weight)
+        return self
+
+    @torch.no_grad()
+    def pack_from_weight(self, keep_weight=False):
+        """RTN-quantize the float weight and pack it in one fused kernel (no LWC/LET)."""
+        wq = self.weight_quantizer
+        group = self._check_packable()
+        if wq.lwc:
+            raise ValueError("pack_from_weight() is plain RTN; use weight_quantizer + pack()")
+        w = self.weight.to(torch.float16).contiguous()
+        out = qlin.quantize(w, wq.n_bits, group, wq._flags(), want_xdq=keep_weight,
+                            want_params=False, pack=True)
+        self._install(out["qweight"], out["scales"], out["zeros"], wq.n_bits, group, keep_weight)
+        if keep_weight:
+            self.weight = out["x_dq"]
+        return self
+
+    def dequantized_weight(self):
+        """W_dq [out, in] fp16 from the packed codes (bit-exact)."""
+        if not self.packed:
+            raise RuntimeError("module is not packed")
+        return qlin.dequant(self.qweight, self.qscales, self.qzeros, self.out_features,
+                            self.in_features, self.wbits, self.group)
+
+    def extra_repr(self):
+        s = f"in_features={self.in_features}, out_features={self.out_features}"
+        if self.packed:
+            s += f", packed=int{self.wbits} g{self.group}"
+        return s

@@ -1,0 +1,53 @@
+"""Norm layers of the quantized decoder layers (reference quant/omni_norm.py:11-63).
+
+Not a kernel target: RMSNorm is computed in fp32 and cast back, exactly as
+the reference does, with torch ops on the device.
+"""
+import torch
+import torch.nn as nn
+
+
+class OmniLayerNorm(nn.Module):
+    def __init__(self, ori_layer_norm) -> None:
+        super().__init__()
+        self.use_act_quant = True
+        self.register_buffer("weight", ori_layer_norm.weight)
+        if ori_layer_norm.bias is not None:
+            self.register_buffer("bias", ori_layer_norm.bias)
+        else:
+            self.bias = None
+        self.eps = ori_layer_norm.eps
+        self.norm_func = nn.functional.layer_norm
+        self.normalized_shape = ori_layer_norm.normalized_shape
+        self.use_temporary_parameter = False
+
+    def forward(self, x):
+        if self.use_temporary_parameter:
+            weight, bias = self.temp_weight, self.temp_bias
+        else:
+            weight, bias = self.weight, self.bias
+        return self.norm_func(x, self.normalized_shape, weight, bias, eps=self.eps)
+
+    def set_quant_state(self, use_weight_quant, use_act_quant):
+        self.use_act_quant = use_act_quant
+
+
+class OmniLlamaRMSNorm(nn.Module):
+    def __init__(self, ori_norm, eps=1e-6):
+        super().__init__()
+        self.register_buffer("weight", ori_norm.weight)
+        self.bias = None
+        self.variance_epsilon = eps
+        self.use_temporary_parameter = False
+
+    def forward(self, hidden_states):
+        input_dtype = hidden_states.dtype
+        variance = hidden_states.to(torch.float32).pow(2).mean(-1, keepdim=True)
+        hidden_states = hidden_states * torch.rsqrt(variance + self.variance_epsilon)
+        if self.use_temporary_parameter:
+            weight, bias = self.temp_weight, self.temp_bias
+        else:
+            weight, bias = self.weight, self.bias
+        if bias is not None:
+            return (weight * hidden_states + bias).to(input_dtype)
+        return (weight * hidden_states).to(input_dtype)

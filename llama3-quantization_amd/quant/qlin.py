@@ -1,0 +1,218 @@
+"""ctypes binding of libqlin_gfx950.so (include/qlin_gfx950.h) — the only door from the Python
+host mirror to the gfx950 kernels.
+
+There is deliberately no fallback: if the library is missing, or a tensor is not on a HIP device,
+every entry point raises.  PyTorch is used here only as the device allocator and for its current
+HIP stream (``torch.cuda`` is PyTorch-ROCm's native HIP backend).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+LIB_NAME = "libqlin_gfx950.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
+                        LIB_NAME)
+ABI_VERSION = 1
+
+SYMMETRIC = 1
+DISABLE_ZERO_POINT = 2
+LWC = 4
+F16 = 0
+F32 = 1
+
+_DT = {torch.float16: F16, torch.float32: F32}
+
+_lock = threading.Lock()
+_lib = None
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_l = ctypes.c_int64
+
+SIGNATURES = {
+    "qlin_abi_version": ([], _i),
+    "qlin_error_string": ([_i], ctypes.c_char_p),
+    "qlin_quantize": ([_p, _i, _l, _l, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p], _i),
+    "qlin_fake_quant": ([_p, _i, _p, _p, _l, _l, _i, _i, _i, _p, _p, _p, _p, _p], _i),
+    "qlin_pack_f16": ([_p, _p, _p, _l, _l, _i, _i, _i, _p, _p, _p, _p], _i),
+    "qlin_dequant_f16": ([_p, _p, _p, _i, _l, _l, _i, _i, _p, _p], _i),
+    "qlin_gemv_f16": ([_p, _p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
+    "qlin_gemm_f16": ([_p, _p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
+    "qlin_linear_f16": ([_p, _p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
+}
+
+
+class QlinError(RuntimeError):
+    pass
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and type the C ABI.  Raises if the library was not built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = path or os.environ.get("QLIN_LIBRARY", LIB_PATH)
+        if not os.path.exists(path):
+            raise QlinError(f"{LIB_NAME} not found at {path}: build it with "
+                            "`python -c 'import __graft_entry__ as g; g.build()'` "
+                            "(make -C llama3-quantization_amd/csrc)")
+        lib = ctypes.CDLL(path)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        v = lib.qlin_abi_version()
+        if v != ABI_VERSION:
+            raise QlinError(f"{path}: ABI version {v}, expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = load_library().qlin_error_string(rc).decode()
+        if rc == 1:
+            raise ValueError(f"{what}: {msg}")
+        raise QlinError(f"{what}: HIP error {rc} ({msg})")
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("qlin kernels run on gfx950 only: got a CPU tensor "
+                               "(no CPU fallback exists)")
+        if not t.is_contiguous():
+            raise ValueError("qlin kernels need contiguous tensors")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _dtcode(t):
+    if t.dtype not in _DT:
+        raise ValueError(f"unsupported dtype {t.dtype} (fp16 / fp32)")
+    return _DT[t.dtype]
+
+
+def quantize(x: torch.Tensor, bits: int, group: int, flags: int = 0, up_sig=None, low_sig=None,
+             want_xdq=True, want_params=True, pack=False):
+    """Fused calibrate + fake-quant (+ pack) of ``x`` viewed as [rows, K]; ``group`` divides K.
+
+    Returns dict with ``x_dq`` [rows, K], ``scale`` / ``zp`` [rows*K/group] and, if ``pack``,
+    ``qweight`` / ``scales`` / ``zeros`` (int16)."""
+    _dev(x, up_sig, low_sig)
+    K = x.shape[-1]
+    rows = x.numel() // K if K else 0
+    out = {}
+    xdq = torch.empty_like(x) if want_xdq else None
+    ng = rows * (K // group) if group else 0
+    scale = torch.empty(ng, dtype=x.dtype, device=x.device) if want_params else None
+    zp = torch.empty(ng, dtype=x.dtype, device=x.device) if (
+        want_params and not flags & DISABLE_ZERO_POINT) else None
+    qw = sc = z16 = None
+    if pack:
+        qw = torch.empty(rows, K * bits // 32, dtype=torch.int32, device=x.device)
+        sc = torch.empty(rows, K // group, dtype=torch.float16, device=x.device)
+        z16 = torch.empty(rows, K // group, dtype=torch.int16, device=x.device)
+    rc = load_library().qlin_quantize(
+        _ptr(x), _dtcode(x), rows, K, bits, group, flags, _ptr(up_sig), _ptr(low_sig),
+        _ptr(xdq), _ptr(scale), _ptr(zp), _ptr(qw), _ptr(sc), _ptr(z16), _stream(x))
+    _check(rc, "qlin_quantize")
+    out.update(x_dq=xdq, scale=scale, zp=zp)
+    if pack:
+        out.update(qweight=qw, scales=sc, zeros=z16)
+    return out
+
+
+def fake_quant(x: torch.Tensor, scale: torch.Tensor, zp, bits: int, group: int, flags: int = 0,
+               want_xdq=True, pack=False):
+    """``fake_quant`` with given (scale, zp) [rows*K/group]; optionally pack the codes."""
+    _dev(x, scale, zp)
+    K = x.shape[-1]
+    rows = x.numel() // K
+    xdq = torch.empty_like(x) if want_xdq else None
+    qw = sc = z16 = None
+    if pack:
+        qw = torch.empty(rows, K * bits // 32, dtype=torch.int32, device=x.device)
+        sc = torch.empty(rows, K // group, dtype=torch.float16, device=x.device)
+        z16 = torch.empty(rows, K // group, dtype=torch.int16, device=x.device)
+    if scale.dtype != x.dtype or (zp is not None and zp.dtype != x.dtype):
+        raise ValueError("scale / zero point dtype must match x")
+    rc = load_library().qlin_fake_quant(
+        _ptr(x), _dtcode(x), _ptr(scale), _ptr(zp), rows, K, bits, group, flags, _ptr(xdq),
+        _ptr(qw), _ptr(sc), _ptr(z16), _stream(x))
+    _check(rc, "qlin_fake_quant")
+    return dict(x_dq=xdq, qweight=qw, scales=sc, zeros=z16)
+
+
+def narrow_zeros(z16: torch.Tensor) -> torch.Tensor:
+    """int16 zero points -> int8 when every value fits (the common case), else keep int16."""
+    if z16.numel() == 0:
+        return z16.to(torch.int8)
+    lo, hi = torch.aminmax(z16)
+    if int(lo) >= -128 and int(hi) <= 127:
+        return z16.to(torch.int8)
+    return z16
+
+
+def zero_bits(zeros: torch.Tensor) -> int:
+    if zeros.dtype == torch.int8:
+        return 8
+    if zeros.dtype == torch.int16:
+        return 16
+    raise ValueError(f"zeros must be int8 / int16, got {zeros.dtype}")
+
+
+def dequant(qweight, scales, zeros, N: int, K: int, bits: int, group: int) -> torch.Tensor:
+    _dev(qweight, scales, zeros)
+    w = torch.empty(N, K, dtype=torch.float16, device=qweight.device)
+    rc = load_library().qlin_dequant_f16(_ptr(qweight), _ptr(scales), _ptr(zeros),
+                                         zero_bits(zeros), N, K, bits, group, _ptr(w),
+                                         _stream(qweight))
+    _check(rc, "qlin_dequant_f16")
+    return w
+
+
+def _linear_call(fn_name, x, qweight, scales, zeros, bias, N, K, bits, group, extra=()):
+    _dev(x, qweight, scales, zeros, bias)
+    if x.dtype != torch.float16:
+        raise ValueError(f"packed linear takes fp16 activations, got {x.dtype}")
+    if x.shape[-1] != K:
+        raise ValueError(f"input has {x.shape[-1]} features, layer expects {K}")
+    if bias is not None and (bias.dtype != torch.float16 or bias.numel() != N):
+        raise ValueError("bias must be fp16 [N]")
+    M = x.numel() // K if K else 0
+    y = torch.empty(*x.shape[:-1], N, dtype=torch.float16, device=x.device)
+    if M == 0:
+        return y
+    fn = getattr(load_library(), fn_name)
+    rc = fn(_ptr(qweight), _ptr(scales), _ptr(zeros), zero_bits(zeros), _ptr(x), _ptr(bias),
+            _ptr(y), M, N, K, bits, group, *extra, _stream(x))
+    _check(rc, fn_name)
+    return y
+
+
+def linear(x, qweight, scales, zeros, bias, N, K, bits, group):
+    """Dispatching fused dequant-matmul (GEMV for M <= 4, MFMA GEMM otherwise)."""
+    return _linear_call("qlin_linear_f16", x, qweight, scales, zeros, bias, N, K, bits, group)
+
+
+def gemv(x, qweight, scales, zeros, bias, N, K, bits, group):
+    return _linear_call("qlin_gemv_f16", x, qweight, scales, zeros, bias, N, K, bits, group)
+
+
+def gemm(x, qweight, scales, zeros, bias, N, K, bits, group):
+    return _linear_call("qlin_gemm_f16", x, qweight, scales, zeros, bias, N, K, bits, group,
+                        extra=(None,))

@@ -1,0 +1,178 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the oracle and the reference's
+golden vectors.  Bit-exact for quantize / pack / dequant; fp16-output tolerance for GEMV / GEMM."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from helpers import assert_close_to_ref, bit_equal, n, rand_weight, rand_x, t
+from oracle import quant_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+from quant import qlin  # noqa: E402
+from quant.quantizer import UniformAffineQuantizer  # noqa: E402
+
+WEIGHT_CASES = ["q_w4g128_f16", "q_w3g64_f16", "q_w2g64_f16", "q_w8pc_f16", "q_w4pc_f16_k4096",
+                "q_w4g128_sym_f16", "q_w4g128_nozp_f16", "q_w8g128_nozp_f16",
+                "q_w4g128_lwc16_f16", "q_w4g128_lwc32_f16", "q_w4g128_f32",
+                "q_w3g64_symlwc_def_f16"]
+
+
+def _params(g):
+    gs = int(g["p_group_size"]) if "p_group_size" in g else -1
+    return dict(n_bits=int(g["p_n_bits"]), group_size=None if gs < 0 else gs,
+                symmetric=bool(g.get("p_symmetric", False)),
+                disable_zero_point=bool(g.get("p_disable_zero_point", False)),
+                lwc=bool(g.get("p_lwc", False)))
+
+
+@pytest.mark.parametrize("name", WEIGHT_CASES)
+def test_quantizer_kernel_matches_reference(name):
+    g = load_golden(name)
+    p = _params(g)
+    W = t(g["w"])
+    q = UniformAffineQuantizer(**p, dynamic_method="per_channel", shape=W.shape).cuda()
+    if p["lwc"]:
+        with torch.no_grad():
+            q.upbound_factor.data = t(g["lwc_up"])
+            q.lowbound_factor.data = t(g["lwc_low"])
+    wdq = q(W)
+    assert bit_equal(n(q.scale), g["scale"]), name
+    if "zp" in g:
+        assert bit_equal(n(q.round_zero_point), g["zp"]), name
+    assert bit_equal(n(wdq), g["w_dq"]), f"{name}: {np.sum(n(wdq) != g['w_dq'])} mismatches"
+
+
+@pytest.mark.parametrize("name", ["q_a8tok_f16", "q_a4tok_f16", "q_a8tok_f32"])
+def test_act_quantizer_kernel_matches_reference(name):
+    g = load_golden(name)
+    q = UniformAffineQuantizer(n_bits=int(g["p_n_bits"]), dynamic_method="per_token").cuda()
+    xdq = q(t(g["x"]))
+    assert bit_equal(n(q.scale), g["scale"]) and bit_equal(n(q.round_zero_point), g["zp"])
+    assert bit_equal(n(xdq), g["x_dq"])
+
+
+def test_fake_quant_given_params_matches_reference():
+    g = load_golden("q_w4g128_f16")
+    q = UniformAffineQuantizer(n_bits=4, group_size=128, dynamic_method="per_channel").cuda()
+    W = t(g["w"])
+    out = q.fake_quant(W, t(g["scale"]), t(g["zp"]))
+    assert bit_equal(n(out), g["w_dq"])
+
+
+PACK_CASES = ["q_w4g128_f16", "q_w3g64_f16", "q_w2g64_f16", "q_w8pc_f16", "q_w4g128_sym_f16",
+              "q_w4g128_nozp_f16", "q_w8g128_nozp_f16", "q_w4pc_f16_k4096"]
+
+
+@pytest.mark.parametrize("name", PACK_CASES)
+def test_pack_and_dequant_bit_exact(name):
+    g = load_golden(name)
+    p = _params(g)
+    N, K = g["w"].shape
+    grp = p["group_size"] or K
+    flags = (qlin.SYMMETRIC if p["symmetric"] else 0) | (
+        qlin.DISABLE_ZERO_POINT if p["disable_zero_point"] else 0)
+    out = qlin.quantize(t(g["w"]), p["n_bits"], grp, flags, pack=True)
+    # oracle packing of the oracle's codes
+    _, scale, zp, x_int = O.quantize(g["w"], p["n_bits"], p["group_size"], p["symmetric"],
+                                     p["disable_zero_point"])
+    ok = ~np.isnan(g["w_dq"]).any(axis=1)
+    oq, osc, oz = O.pack_from_quant(np.nan_to_num(x_int), scale, zp, p["n_bits"], N, K,
+                                    p["group_size"], p["disable_zero_point"])
+    assert np.array_equal(n(out["qweight"]).view(np.uint32)[ok], oq[ok])
+    assert bit_equal(n(out["scales"]), osc)
+    assert np.array_equal(n(out["zeros"]).astype(np.int32), oz.astype(np.int32))
+    z = qlin.narrow_zeros(out["zeros"])
+    w = qlin.dequant(out["qweight"], out["scales"], z, N, K, p["n_bits"], grp)
+    assert bit_equal(n(w)[ok], g["w_dq"][ok])
+    # the real-quant packer: codes recovered from (W_dq, scales, zeros) alone
+    wdq = np.where(ok[:, None], g["w_dq"], 0).astype(np.float16)
+    pz = None if p["disable_zero_point"] else t(g["zp"].reshape(-1))
+    out2 = qlin.fake_quant(t(wdq), t(g["scale"].reshape(-1)), pz, p["n_bits"], grp,
+                           flags & qlin.DISABLE_ZERO_POINT, want_xdq=False, pack=True)
+    w2 = qlin.dequant(out2["qweight"], out2["scales"], qlin.narrow_zeros(out2["zeros"]), N, K,
+                      p["n_bits"], grp)
+    assert bit_equal(n(w2)[ok], g["w_dq"][ok])
+
+
+def _packed(N, K, bits, group, seed, wide=False):
+    W = rand_weight(N, K, seed)
+    if wide:
+        W[: max(1, N // 7), :group] = 1.0 + np.random.RandomState(seed).rand(
+            max(1, N // 7), group).astype(np.float16) * np.float16(1e-3)
+    out = qlin.quantize(t(W), bits, group, 0, pack=True)
+    z = qlin.narrow_zeros(out["zeros"])
+    wdq = n(qlin.dequant(out["qweight"], out["scales"], z, N, K, bits, group))
+    return out["qweight"], out["scales"], z, wdq
+
+
+GEMV_SHAPES = [(4096, 4096, 128), (1024, 4096, 128), (777, 768, 128), (300, 3072, 64),
+               (130, 14336, 128), (64, 32, 32), (96, 512, 512)]
+
+
+@pytest.mark.parametrize("bits", [4, 3, 2, 8])
+@pytest.mark.parametrize("shape", GEMV_SHAPES)
+def test_gemv_matches_oracle(bits, shape):
+    N, K, group = shape
+    if bits in (2, 3) and group == 128:
+        group = 64 if K % 64 == 0 else group
+    qw, sc, z, wdq = _packed(N, K, bits, group, seed=N + K + bits)
+    bias = np.random.RandomState(3).randn(N).astype(np.float16) * np.float16(0.1)
+    for M in (1, 2, 3, 4):
+        x = rand_x(M, K, seed=M)
+        for b in (None, bias):
+            y = qlin.gemv(t(x), qw, sc, z, None if b is None else t(b), N, K, bits, group)
+            ref = O.linear_ref(x, wdq, b)
+            assert_close_to_ref(n(y), ref, what=f"gemv b{bits} M{M} N{N} K{K} g{group}")
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_gemv_wide_zeros(wide):
+    N, K, group = 512, 1024, 128
+    qw, sc, z, wdq = _packed(N, K, 4, group, seed=5, wide=wide)
+    assert (z.dtype == torch.int16) == wide
+    x = rand_x(1, K, 9)
+    y = qlin.gemv(t(x), qw, sc, z, None, N, K, 4, group)
+    assert_close_to_ref(n(y), O.linear_ref(x, wdq), what="wide")
+
+
+GEMM_SHAPES = [(5, 4096, 4096, 128), (33, 1024, 4096, 128), (128, 777, 768, 128),
+               (300, 256, 3072, 64), (200, 4096, 14336, 128), (2048, 512, 1024, 128)]
+
+
+@pytest.mark.parametrize("bits", [4, 3, 2, 8])
+@pytest.mark.parametrize("shape", GEMM_SHAPES)
+def test_gemm_matches_oracle(bits, shape):
+    M, N, K, group = shape
+    if bits in (2, 3) and group == 128:
+        group = 64
+    qw, sc, z, wdq = _packed(N, K, bits, group, seed=M + N + K + bits)
+    x = rand_x(M, K, seed=M)
+    bias = np.random.RandomState(4).randn(N).astype(np.float16) * np.float16(0.1)
+    y = qlin.gemm(t(x), qw, sc, z, t(bias), N, K, bits, group)
+    assert_close_to_ref(n(y), O.linear_ref(x, wdq, bias), what=f"gemm b{bits} {shape}")
+
+
+def test_linear_dispatch_and_batch_shapes():
+    N, K, group = 384, 1024, 128
+    qw, sc, z, wdq = _packed(N, K, 4, group, seed=11)
+    for shp in ((1, 1, K), (1, 3, K), (2, 5, K), (1, 64, K)):
+        x = np.random.RandomState(len(shp)).randn(*shp).astype(np.float16)
+        y = qlin.linear(t(x), qw, sc, z, None, N, K, 4, group)
+        assert tuple(y.shape) == shp[:-1] + (N,)
+        assert_close_to_ref(n(y).reshape(-1, N), O.linear_ref(x.reshape(-1, K), wdq))
+
+
+def test_invalid_arguments_raise():
+    N, K, group = 64, 256, 128
+    qw, sc, z, _ = _packed(N, K, 4, group, seed=1)
+    x = t(rand_x(1, K, 1))
+    with pytest.raises(ValueError):
+        qlin.gemv(x, qw, sc, z, None, N, K, 5, group)          # bits
+    with pytest.raises(ValueError):
+        qlin.gemv(x, qw, sc, z, None, N, K, 4, 100)            # group
+    with pytest.raises(ValueError):
+        qlin.linear(x.float(), qw, sc, z, None, N, K, 4, group)  # dtype
+    with pytest.raises(RuntimeError):
+        qlin.linear(x.cpu(), qw, sc, z, None, N, K, 4, group)    # CPU tensor: no fallback

@@ -1,0 +1,116 @@
+"""CPU-side checks: the C-ABI library loads and exports every declared symbol, argument
+validation fails cleanly without a GPU, and the host mirror keeps the reference module API."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "qlin_gfx950.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(qlin_\w+)\s*\(", src)))
+
+
+def test_header_declares_the_abi():
+    syms = declared_symbols()
+    for s in ("qlin_quantize", "qlin_fake_quant", "qlin_pack_f16", "qlin_dequant_f16",
+              "qlin_gemv_f16", "qlin_gemm_f16", "qlin_linear_f16", "qlin_abi_version",
+              "qlin_error_string"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from quant import qlin
+    lib = qlin.load_library()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+        assert s in qlin.SIGNATURES, f"binding lacks {s}"
+    assert lib.qlin_abi_version() == qlin.ABI_VERSION
+
+
+def test_invalid_arguments_return_einval_without_a_gpu():
+    from quant import qlin
+    lib = qlin.load_library()
+    # every entry point validates before touching the device
+    assert lib.qlin_dequant_f16(None, None, None, 8, 16, 64, 4, 64, None, None) == 1
+    assert lib.qlin_gemv_f16(None, None, None, 8, None, None, None, 1, 16, 64, 4, 64, None) == 1
+    assert lib.qlin_gemm_f16(None, None, None, 8, None, None, None, 8, 16, 64, 4, 64, None, None) == 1
+    assert lib.qlin_quantize(None, 0, 4, 64, 4, 64, 0, None, None, None, None, None, None, None,
+                             None, None) == 1
+    p = ctypes.c_void_p(16)  # never dereferenced: the shape check fails first
+    assert lib.qlin_gemv_f16(p, p, p, 8, p, None, p, 1, 16, 65, 4, 64, None) == 1   # K % 32
+    assert lib.qlin_gemv_f16(p, p, p, 8, p, None, p, 9, 16, 64, 4, 64, None) == 1   # M > 4
+    assert lib.qlin_gemv_f16(p, p, p, 8, p, None, p, 1, 16, 64, 5, 64, None) == 1   # bits
+    assert lib.qlin_gemv_f16(p, p, p, 12, p, None, p, 1, 16, 64, 4, 64, None) == 1  # zero bits
+    assert lib.qlin_error_string(1) == b"invalid argument"
+
+
+def test_reference_module_api_is_kept():
+    from quant.int_linear import QuantLinear
+    from quant.int_matmul import QuantMatMul
+    from quant.quantizer import UniformAffineQuantizer
+    lin = torch.nn.Linear(256, 64, bias=True)
+    q = QuantLinear(lin, dict(n_bits=4, group_size=128, dynamic_method="per_channel",
+                              per_channel_axes=[0], lwc=True),
+                    dict(n_bits=8, dynamic_method="per_token"))
+    # buffers alias the original module (quant/int_linear.py:26-30)
+    assert q.weight.data_ptr() == lin.weight.data_ptr()
+    assert q.bias.data_ptr() == lin.bias.data_ptr()
+    for a in ("in_features", "out_features", "weight_quantizer", "act_quantizer",
+              "use_weight_quant", "use_act_quant", "use_temporary_parameter", "fwd_func",
+              "fwd_kwargs", "disable_input_quant"):
+        assert hasattr(q, a), a
+    q.set_quant_state(weight_quant=True, act_quant=True)
+    assert q.use_weight_quant and q.use_act_quant
+    wq = q.weight_quantizer
+    assert isinstance(wq, UniformAffineQuantizer)
+    assert (wq.qmin, wq.qmax) == (0, 15)
+    assert wq.upbound_factor.shape == (64 * 2, 1) and float(wq.upbound_factor[0]) == 4.0
+    wq.change_n_bits(3)
+    assert wq.qmax == 7
+    sym = UniformAffineQuantizer(n_bits=4, disable_zero_point=True)
+    assert (sym.qmin, sym.qmax) == (-8, 7)
+    with pytest.raises(AssertionError):
+        UniformAffineQuantizer(n_bits=17)
+    # dense (unquantized) forward is the reference's F.linear
+    x = torch.randn(2, 256)
+    q.set_quant_state(False, False)
+    torch.testing.assert_close(q(x), torch.nn.functional.linear(x, lin.weight, lin.bias))
+    mm = QuantMatMul(matmul_func=torch.matmul)
+    a, b = torch.randn(2, 3, 4), torch.randn(2, 4, 5)
+    torch.testing.assert_close(mm(mm.quant_x1(a), mm.quant_x2(b)), a @ b)
+
+
+def test_quantizer_bypass_and_errors_match_reference():
+    from quant.quantizer import UniformAffineQuantizer
+    x = torch.randn(4, 64)
+    assert UniformAffineQuantizer(n_bits=16)(x) is x            # quantizer.py:119-120
+    q = UniformAffineQuantizer(n_bits=4)
+    q.enable = False
+    assert q(x) is x
+    with pytest.raises(NotImplementedError):                    # quantizer.py:124-127
+        UniformAffineQuantizer(n_bits=4, dynamic_method="per_cluster")(x)
+
+
+def test_no_cpu_fallback():
+    """The product path refuses CPU tensors instead of silently computing on the host."""
+    from quant.quantizer import UniformAffineQuantizer
+    q = UniformAffineQuantizer(n_bits=4, group_size=32, dynamic_method="per_channel")
+    with pytest.raises(RuntimeError, match="gfx950"):
+        q(torch.randn(4, 64).half())
+
+
+def test_product_path_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "llama3-quantization_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in src.replace("oracle/", ""), f

@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprof kernel-trace summary.
+# Stops at the first crash / fault / timeout (exit codes other than 0 and pytest's 1).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+ok_or_stop() {  # $1 = rc, $2 = step
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "STOP: $2 exited $1"; exit "$1"; fi
+}
+STEPS="${STEPS:-tests smoke bench prof}"
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+      rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"; ok_or_stop $rc pytest ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -2 "$OUT/smoke.log"; ok_or_stop $rc smoke ;;
+    bench)
+      timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
+      rc=$?; echo "bench rc=$rc"; tail -3 "$OUT/bench.log"; ok_or_stop $rc bench ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
+         -- python "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/prof.log" 2>&1)
+      rc=$?; echo "prof rc=$rc"; tail -3 "$OUT/prof.log"; ok_or_stop $rc prof
+      find "$OUT/prof" -name "*kernel_stats.csv" -exec head -20 {} \; ;;
+  esac
+done
