@@ -41,8 +41,9 @@ WORKLOADS = {
 }
 
 
-def algo_bytes(M, N, K, bits, group, zero_bytes=1):
-    """2MK + N*K*bits/8 + N*(K/g)*(2 + zb) + 2MN."""
+def algo_bytes(M, N, K, bits, group, zero_bytes=2):
+    """2MK + N*K*bits/8 + N*(K/g)*(2 + zb) + 2MN; the qsz layout stores each
+    group's fp16 scale and int16 zero point in one 32-bit word (zb = 2)."""
     return 2 * M * K + N * K * bits // 8 + N * (K // group) * (2 + zero_bytes) + 2 * M * N
 
 
@@ -125,32 +126,29 @@ def main():
     R = args.ring or ring
     gen = torch.Generator(device=dev)
     mats = []
-    zb = 1
+    zb = 2
     for i in range(R):
         gen.manual_seed(1_000_003 * rank + i)
         w = torch.empty(N, K, device=dev, dtype=torch.float16).normal_(0.0, 0.02, generator=gen)
         o = qlin.quantize(w, bits, group, 0, want_xdq=False, want_params=False, pack=True)
-        z = qlin.narrow_zeros(o["zeros"])
-        zb = z.element_size()
-        mats.append((o["qweight"], o["scales"], z))
+        mats.append((o["qweight"], o["qsz"], o["flags"]))
         del w, o
     gen.manual_seed(1234)
     x = torch.empty(M, K, device=dev, dtype=torch.float16).normal_(0.0, 1.0, generator=gen)
     ys = [torch.empty(M, N, device=dev, dtype=torch.float16) for _ in range(min(R, 4))]
     lib = qlin.load_library()
     fn = lib.qlin_gemv_f16 if kernel == "gemv" else lib.qlin_gemm_f16
-    zbits = 8 * zb
 
     def step():
         st = torch.cuda.current_stream(dev).cuda_stream
-        for i, (qw, sc, z) in enumerate(mats):
+        for i, (qw, qsz, fl) in enumerate(mats):
             y = ys[i % len(ys)]
             if kernel == "gemv":
-                rc = fn(qw.data_ptr(), sc.data_ptr(), z.data_ptr(), zbits, x.data_ptr(), None,
-                        y.data_ptr(), M, N, K, bits, group, st)
+                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl, x.data_ptr(), None, y.data_ptr(),
+                        M, N, K, bits, group, st)
             else:
-                rc = fn(qw.data_ptr(), sc.data_ptr(), z.data_ptr(), zbits, x.data_ptr(), None,
-                        y.data_ptr(), M, N, K, bits, group, None, st)
+                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl, x.data_ptr(), None, y.data_ptr(),
+                        M, N, K, bits, group, None, st)
             if rc != 0:
                 raise RuntimeError(f"kernel failed: {rc}")
 
@@ -228,7 +226,7 @@ def main():
         "data": "synthetic",
         "hbm_GBps_total": round(nbytes * launches * world / elapsed / 1e9, 1),
         "config": {"workload": args.workload, "note": note, "M": M, "N": N, "K": K,
-                   "bits": bits, "group_size": group, "ring": R, "zero_bits": 8 * zb,
+                   "bits": bits, "group_size": group, "ring": R, "sz_bytes_per_group": 2 + zb,
                    "graph": use_graph, "parallelism": f"weak x{world} (independent rings)"},
         "roofline": roof,
         "wall_s": round(wall, 4),

@@ -15,13 +15,23 @@
  *   - stateless and reentrant; safe to call from any host thread and inside stream capture.
  *   - fp16 tensors are passed as uint16_t* (IEEE binary16 bit patterns).
  *
- * Canonical packed weight layout ("qlin" layout):
- *   qweight  uint32 [N, K*bits/32]  K-packed per output row in 32-element lane chunks of `bits`
- *            words; bits in {2,3,4,8}.  Element order inside a chunk: oracle/quant_oracle.py header.
- *   scales   fp16   [N, K/group]    == reference scales.view(N, -1)     (quant/omniquant.py:322-325)
- *   zeros    int8 or int16 [N, K/group] (zero_bits = 8 | 16), integral zero point
- *            == reference zeros.view(N, -1); disable_zero_point is stored as zero = 2^(bits-1).
+ * Canonical packed weight layout ("qlin tiled" layout):
+ *   qweight  uint32 [ceil(N/16), ceil(K/128), 64, bits]: 16-row x 128-k tiles of 64 lane pieces;
+ *            lane l = n + 16q of a tile holds the 32 codes of tile row n at k = 32s + 8q + j
+ *            (s < 4, j < 8) — the B operand of v_mfma_f32_16x16x32_f16 k-step s.  bits in
+ *            {2,3,4,8}; bit positions inside a piece: oracle/quant_oracle.py pack_qweight and
+ *            llama3-quantization_amd/csrc/qlin_common.h.  Codes of rows >= N / k >= K are
+ *            ignored (the packers write k >= K as 0; rows >= N are never written).
+ *   qsz      uint32 [ceil(N/16), K/group, 16]: the (scale, zero) of row 16*nt + n, group g at
+ *            [nt][g][n] — fp16 scale in bits 0..15 (== reference scales.view(N, -1),
+ *            quant/omniquant.py:322-325), int16 integral zero point in bits 16..31 (== reference
+ *            zeros.view(N, -1); disable_zero_point is stored as zero = 2^(bits-1)).  One 64-byte
+ *            coalesced load gives a tile's 16 rows their group parameters.
+ *   flags    QLIN_WIDE_ZERO when some |zero| > 1024 (possible only for degenerate groups: the
+ *            reference clamps zero points to +-1e4), selecting the fp32 (u - zero) path.
  *   group    multiple of 32 dividing K (group = K for per-channel); K % 32 == 0.
+ * Both arrays must be allocated padded (ceil(N/16)*16 rows, ceil(K/128)*128 codes) and zeroed
+ * before packing; the packers write rows < N only.
  */
 #ifndef QLIN_GFX950_H
 #define QLIN_GFX950_H
@@ -32,12 +42,14 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 1
+#define QLIN_ABI_VERSION 2
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
 #define QLIN_DISABLE_ZERO_POINT 2
 #define QLIN_LWC                4
+/* packed-layout flag (dequant / GEMV / GEMM entry points) */
+#define QLIN_WIDE_ZERO          8
 
 /* element dtypes */
 #define QLIN_F16 0
@@ -58,13 +70,12 @@ const char* qlin_error_string(int code);
  *   x_dq       [rows, K] dtype or NULL;  scale_out / zp_out [rows*K/group] dtype or NULL
  *              (zp_out unused with QLIN_DISABLE_ZERO_POINT) — the reference's scale /
  *              round_zero_point tensors.
- *   qweight, scales, zeros16: canonical packed outputs (dtype must be QLIN_F16), or all NULL;
- *              zeros are always written as int16 here (narrow to int8 on the host if they fit).
+ *   qweight, qsz: canonical packed outputs (dtype must be QLIN_F16), or both NULL.
  */
 int qlin_quantize(const void* x, int dtype, int64_t rows, int64_t K, int bits, int group,
                   int flags, const void* lwc_up_sig, const void* lwc_low_sig,
                   void* x_dq, void* scale_out, void* zp_out,
-                  uint32_t* qweight, uint16_t* scales, int16_t* zeros16, void* stream);
+                  uint32_t* qweight, uint32_t* qsz, void* stream);
 
 /*
  * fake_quant with given parameters (quant/quantizer.py:94-115): x_dq = RN(RN(clamp(round_ste(
@@ -74,7 +85,7 @@ int qlin_quantize(const void* x, int dtype, int64_t rows, int64_t K, int bits, i
  */
 int qlin_fake_quant(const void* x, int dtype, const void* scale, const void* zp, int64_t rows,
                     int64_t K, int bits, int group, int flags, void* x_dq, uint32_t* qweight,
-                    uint16_t* scales, int16_t* zeros16, void* stream);
+                    uint32_t* qsz, void* stream);
 
 /*
  * Real-quant packer: canonical layout from (W_dq, scales, zeros) as registered by
@@ -87,36 +98,34 @@ int qlin_fake_quant(const void* x, int dtype, const void* scale, const void* zp,
  */
 int qlin_pack_f16(const uint16_t* w_dq, const uint16_t* scales_ref, const uint16_t* zeros_ref,
                   int64_t N, int64_t K, int bits, int group, int flags,
-                  uint32_t* qweight, uint16_t* scales, int16_t* zeros16, void* stream);
+                  uint32_t* qweight, uint32_t* qsz, void* stream);
 
 /*
  * Dequantize the canonical layout: w[n,k] = RN16(RN16(q - zp) * s), bit-exact with the reference
  * fake_quant's x_dequant.sub(zp).mul(scale) (quant/quantizer.py:107-110).  Debug / parity and
  * the fake-quant eval mode (module.weight = W_dq, quant/utils.py:133-136).
  */
-int qlin_dequant_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
-                     int zero_bits, int64_t N, int64_t K, int bits, int group, uint16_t* w,
-                     void* stream);
+int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, int64_t N,
+                     int64_t K, int bits, int group, uint16_t* w, void* stream);
 
 /*
  * y[M, N] = x[M, K] @ W_dq[N, K]^T (+ bias[N]) with the group-wise unpack + dequant fused into the
  * product; fp16 in/out, fp32 accumulation.  Replaces QuantLinear.forward's
  * fwd_func(input, weight, bias) = F.linear (quant/int_linear.py:62) on packed weights.
- *   qlin_gemv_f16: wave64 GEMV, 1 <= M <= 4 (decode).
+ *   qlin_gemv_f16: matrix-core GEMV, 1 <= M <= 4 (decode).
  *   qlin_gemm_f16: MFMA (v_mfma_f32_*_f16) tiles, any M >= 1 (prefill / PPL windows).
  *   qlin_linear_f16: picks one of the two from M.
  *   workspace: reserved, pass NULL.
  */
-int qlin_gemv_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
-                  int zero_bits, const uint16_t* x, const uint16_t* bias, uint16_t* y,
-                  int64_t M, int64_t N, int64_t K, int bits, int group, void* stream);
-int qlin_gemm_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
-                  int zero_bits, const uint16_t* x, const uint16_t* bias, uint16_t* y,
-                  int64_t M, int64_t N, int64_t K, int bits, int group, void* workspace,
-                  void* stream);
-int qlin_linear_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
-                    int zero_bits, const uint16_t* x, const uint16_t* bias, uint16_t* y,
-                    int64_t M, int64_t N, int64_t K, int bits, int group, void* stream);
+int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
+                  const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
+                  int group, void* stream);
+int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
+                  const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
+                  int group, void* workspace, void* stream);
+int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
+                    const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
+                    int group, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,10 +1,21 @@
 // qlin_common.h — device helpers shared by the gfx950 quantized-linear kernels.
 //
-// Written for CDNA4 (gfx950, wave64) only.  The fp16 unpack uses the "magic number" form: a code u
-// placed in the low mantissa bits of 0x6400 (= 1024.0h) gives the fp16 value 1024 + u exactly, so
-// (1024 + u) - (1024 + zp) is the exact integer u - zp in fp16 (Sterbenz), and one v_pk_mul_f16 by
-// the group scale rounds once — bit-identical to the reference's fp16
-// x_dequant.sub(round_zero_point).mul(scale) (quant/quantizer.py:107-110).
+// Written for CDNA4 (gfx950, wave64) only.
+//
+// Packed layout ("qlin tiled", include/qlin_gfx950.h): qweight is a grid of 16-row x 128-k tiles;
+// a tile is 64 lane pieces of BITS uint32.  Lane l = n + 16q holds the 32 codes (s, j), s < 4,
+// j < 8, of tile row n at k = 32s + 8q + j, i.e. exactly the B operand that lane feeds to k-step s
+// of v_mfma_f32_16x16x32_f16 (B[k = 8q + j][col n]).  A GEMV wave therefore streams one fully
+// coalesced 64 x (4*BITS)-byte load per tile and needs no shuffles.
+//
+// Unpack: codes sit in each 16-bit half so that ONE v_and_or_b32 with an fp16 exponent "magic"
+// (1024, 256, 64 or 16, chosen so the code's weight in the mantissa is exactly 1) turns a pair of
+// codes into the fp16 pair (off + u_j, off + u_j+1).  Two uses:
+//   exact dequant: (off + u) - (off + zp) is the exact integer u - zp, and one v_pk_mul_f16 by the
+//     group scale rounds once — bit-identical to the reference's fp16
+//     x_dequant.sub(round_zero_point).mul(scale) (quant/quantizer.py:107-110);
+//   GEMV: the MFMA consumes (off + u) directly; sum_k (off_k + u_k - off_k - zp) x_k * s is
+//     recovered per group from two per-group x sums (S1 = sum off_k x_k, S2 = sum x_k).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -16,6 +27,9 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int kTileN = 16;
+constexpr int kTileK = 128;
 
 __device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
 __device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -38,98 +52,158 @@ __device__ __forceinline__ float min_nan(float a, float b) { return (a != a || b
 __device__ __forceinline__ float max_nan(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : fmaxf(a, b); }
 
 // ---------------------------------------------------------------------------------------------
-// canonical layout: one 32-element lane chunk = BITS uint32 words
+// tiled layout
 // ---------------------------------------------------------------------------------------------
-template <int BITS> struct Chunk { uint32_t w[BITS]; };
+template <int BITS> struct Piece { uint32_t w[BITS]; };
+
+// word offset of lane piece (nt, kt, lane)
+__device__ __forceinline__ int64_t piece_off(int64_t nt, int kt, int Kt, int lane, int bits) {
+  return ((nt * Kt + kt) * 64 + lane) * bits;
+}
 
 template <int BITS>
-__device__ __forceinline__ Chunk<BITS> load_chunk(const uint32_t* __restrict__ p) {
-  Chunk<BITS> c;
+__device__ __forceinline__ Piece<BITS> load_piece(const uint32_t* __restrict__ p) {
+  Piece<BITS> c;
   if constexpr (BITS == 4) {
-    uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
     c.w[0] = v.x; c.w[1] = v.y; c.w[2] = v.z; c.w[3] = v.w;
   } else if constexpr (BITS == 8) {
-    uint4 a = *reinterpret_cast<const uint4*>(p);
-    uint4 b = *reinterpret_cast<const uint4*>(p + 4);
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
     c.w[0] = a.x; c.w[1] = a.y; c.w[2] = a.z; c.w[3] = a.w;
     c.w[4] = b.x; c.w[5] = b.y; c.w[6] = b.z; c.w[7] = b.w;
   } else if constexpr (BITS == 2) {
-    uint2 v = *reinterpret_cast<const uint2*>(p);
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
     c.w[0] = v.x; c.w[1] = v.y;
-  } else {  // BITS == 3: 12 bytes, 4-byte aligned
+  } else {  // 3: 12 bytes, 4-byte aligned -> global_load_dwordx3
     struct U3 { uint32_t a, b, c; };
-    U3 v = *reinterpret_cast<const U3*>(p);
+    const U3 v = *reinterpret_cast<const U3*>(p);
     c.w[0] = v.a; c.w[1] = v.b; c.w[2] = v.c;
   }
   return c;
 }
 
-// 0x64006400 (fp16 pair 1024, 1024) held in a VGPR: gfx9 VOP3 cannot encode a literal, so with
-// the constant opaque to the optimiser (w & mask) | magic selects ONE v_and_or_b32 (mask in an
-// SGPR) instead of a v_and_b32 + v_or_b32 literal pair.
-__device__ __forceinline__ uint32_t magic_vgpr() {
-  uint32_t m;
-  asm("v_mov_b32 %0, 0x64006400" : "=v"(m));
-  return m;
+// int3 high-bit word rotation per k-step (oracle/quant_oracle.py RHO3)
+__host__ __device__ constexpr int rho3(int s) { return s == 0 ? 0 : s == 1 ? 1 : s == 2 ? 8 : 9; }
+
+// fp16 offset of pair P (codes j = 2P, 2P+1) of a k-step
+template <int BITS> __host__ __device__ constexpr int pair_off(int P) {
+  return BITS == 8 ? 1024 : BITS == 4 ? ((P & 1) ? 64 : 1024)
+                                      : (P == 0 ? 1024 : P == 1 ? 256 : P == 2 ? 64 : 16);
 }
 
-// fp16 pair (1024 + u[2p], 1024 + u[2p+1]) of pair index p (0..15) of a chunk, as raw bits
-template <int BITS, int P>
-__device__ __forceinline__ uint32_t magic_pair(const Chunk<BITS>& c, uint32_t magic) {
-  static_assert(P >= 0 && P < 16, "pair index");
+// An fp16-pair constant kept in a VGPR.  gfx9 VOP3 has no literal operand, so with the constant
+// opaque to the optimiser `(w & mask) | magic` selects ONE v_and_or_b32 (mask from an SGPR).
+template <uint32_t C>
+__device__ __forceinline__ uint32_t vreg() {
+  uint32_t m;
+  asm("v_mov_b32 %0, %1" : "=v"(m) : "i"(C));
+  return m;
+}
+struct Magics {
+  uint32_t m1024, m256, m64, m16;
+};
+template <int BITS>
+__device__ __forceinline__ Magics make_magics() {
+  Magics g;
+  g.m1024 = vreg<0x64006400u>();
+  g.m64 = (BITS != 8) ? vreg<0x54005400u>() : 0u;
+  g.m256 = (BITS == 2 || BITS == 3) ? vreg<0x5C005C00u>() : 0u;
+  g.m16 = (BITS == 2 || BITS == 3) ? vreg<0x4C004C00u>() : 0u;
+  return g;
+}
+
+// raw (off + u) fp16 pairs of k-step S of a lane piece: v[P] = pair (j = 2P, 2P+1)
+template <int BITS, int S>
+__device__ __forceinline__ void step_pairs(const Piece<BITS>& c, const Magics& g, uint32_t (&v)[4]) {
   if constexpr (BITS == 4) {
-    return ((c.w[P >> 2] >> (4 * (P & 3))) & 0x000F000Fu) | magic;
+    const uint32_t w = c.w[S];
+    const uint32_t w8 = w >> 8;
+    v[0] = (w & 0x000F000Fu) | g.m1024;
+    v[1] = (w & 0x00F000F0u) | g.m64;
+    v[2] = (w8 & 0x000F000Fu) | g.m1024;
+    v[3] = (w8 & 0x00F000F0u) | g.m64;
   } else if constexpr (BITS == 8) {
-    return ((c.w[P >> 1] >> (8 * (P & 1))) & 0x00FF00FFu) | magic;
-  } else if constexpr (BITS == 2) {
-    return ((c.w[P >> 3] >> (2 * (P & 7))) & 0x00030003u) | magic;
+    const uint32_t a = c.w[2 * S], b = c.w[2 * S + 1];
+    v[0] = (a & 0x00FF00FFu) | g.m1024;
+    v[1] = ((a >> 8) & 0x00FF00FFu) | g.m1024;
+    v[2] = (b & 0x00FF00FFu) | g.m1024;
+    v[3] = ((b >> 8) & 0x00FF00FFu) | g.m1024;
   } else {
-    const uint32_t lo = ((c.w[P >> 3] >> (2 * (P & 7))) & 0x00030003u) | magic;
-    uint32_t hi;
-    if constexpr (P >= 2) hi = c.w[2] >> (P - 2);
-    else hi = c.w[2] << (2 - P);
-    return (hi & 0x00040004u) | lo;
+    const uint32_t w = (S & 1) ? (c.w[S >> 1] >> 8) : c.w[S >> 1];
+    v[0] = (w & 0x00030003u) | g.m1024;
+    v[1] = (w & 0x000C000Cu) | g.m256;
+    v[2] = (w & 0x00300030u) | g.m64;
+    v[3] = (w & 0x00C000C0u) | g.m16;
+    if constexpr (BITS == 3) {
+      const uint32_t h = (rho3(S) == 0) ? c.w[2] : __builtin_amdgcn_alignbit(c.w[2], c.w[2], rho3(S));
+      v[0] |= h & 0x00040004u;
+      v[1] |= h & 0x00100010u;
+      v[2] |= h & 0x00400040u;
+      v[3] |= h & 0x01000100u;
+    }
   }
 }
 
-// per-group dequant constants
+// packed (scale, zero) word of the qsz array [ceil(N/16), G, 16]: fp16 scale in bits 0..15,
+// int16 zero point in bits 16..31
+__device__ __forceinline__ int64_t sz_index(int64_t nt, int g, int G, int n) {
+  return (nt * G + g) * kTileN + n;
+}
+__device__ __forceinline__ _Float16 sz_scale(uint32_t w) {
+  return __builtin_bit_cast(_Float16, (uint16_t)(w & 0xFFFFu));
+}
+__device__ __forceinline__ int sz_zero(uint32_t w) { return (int)(int16_t)(w >> 16); }
+__device__ __forceinline__ uint32_t sz_pack(_Float16 s, int z) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, s) | ((uint32_t)(uint16_t)(int16_t)z << 16);
+}
+
+// per-group dequant constants for the exact path
 struct GroupQ {
-  uint32_t magic;  // 0x64006400 in a VGPR
-  h2 ss;    // (s, s)
-  h2 zz;    // (1024 + zp, 1024 + zp)   narrow zeros
-  float zf; // zp                       wide zeros
+  h2 ss;     // (s, s)
+  h2 zz[4];  // (off_P + zp) pairs, narrow zeros
+  float zf;  // zp, wide zeros
 };
 
-template <bool WIDE>
+template <int BITS, bool WIDE>
 __device__ __forceinline__ GroupQ make_group(_Float16 s, int zp) {
   GroupQ g;
-  g.magic = magic_vgpr();
   g.ss = h2{s, s};
   if constexpr (!WIDE) {
-    const _Float16 z = (_Float16)(1024 + zp);  // exact: |zp| <= 128
-    g.zz = h2{z, z};
+#pragma unroll
+    for (int P = 0; P < 4; ++P) {
+      const _Float16 z = (_Float16)(pair_off<BITS>(P) + zp);  // exact: |zp| <= 1024
+      g.zz[P] = h2{z, z};
+    }
   } else {
     g.zf = (float)zp;
   }
   return g;
 }
 
-// dequantized fp16 pair P of a chunk: RN16(RN16(u - zp) * s), bit-exact with the reference
-template <int BITS, bool WIDE, int P>
-__device__ __forceinline__ h2 dequant_pair(const Chunk<BITS>& c, const GroupQ& g) {
+// exact dequantized fp16 values of k-step S: out[P] = (w_2P, w_2P+1) = RN16(RN16(u - zp) * s)
+template <int BITS, bool WIDE, int S>
+__device__ __forceinline__ void dequant_step(const Piece<BITS>& c, const Magics& mg, const GroupQ& g,
+                                             uint32_t (&out)[4]) {
 #pragma clang fp contract(off)
-  const h2 q = as_h2(magic_pair<BITS, P>(c, g.magic));
-  h2 d;
-  if constexpr (!WIDE) {
-    d = q - g.zz;  // exact integer u - zp
-  } else {
-    // |zp| up to 1e4: u - zp is formed exactly in fp32 and rounded once to fp16, as the
-    // reference's fp16 x_int.sub(round_zero_point) does
-    const float lo = ((float)q.x - 1024.0f) - g.zf;
-    const float hi = ((float)q.y - 1024.0f) - g.zf;
-    d = h2{(_Float16)lo, (_Float16)hi};
+  uint32_t v[4];
+  step_pairs<BITS, S>(c, mg, v);
+#pragma unroll
+  for (int P = 0; P < 4; ++P) {
+    const h2 q = as_h2(v[P]);
+    h2 d;
+    if constexpr (!WIDE) {
+      d = q - g.zz[P];  // exact integer u - zp
+    } else {
+      // |zp| > 1024 (up to 1e4, QLIN_WIDE_ZERO): u - zp formed exactly in fp32, rounded once to
+      // fp16 as the reference's fp16 x_int.sub(round_zero_point) does
+      const float off = (float)pair_off<BITS>(P);
+      const float lo = ((float)q.x - off) - g.zf;
+      const float hi = ((float)q.y - off) - g.zf;
+      d = h2{(_Float16)lo, (_Float16)hi};
+    }
+    out[P] = as_u32(d * g.ss);
   }
-  return d * g.ss;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -148,16 +222,6 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f<0x141>(v);  // row_half_mirror
   v += dpp_f<0x140>(v);  // row_mirror
   return v;
-}
-
-// wave-uniform total over all 64 lanes (requires EXEC all ones)
-__device__ __forceinline__ float wave_sum(float v) {
-  v = row16_sum(v);
-  const int b = __builtin_bit_cast(int, v);
-  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
-          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
-         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
-          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
 }
 
 }  // namespace qlin

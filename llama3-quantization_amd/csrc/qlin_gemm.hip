@@ -3,11 +3,12 @@
 // y[M, N] = x[M, K] @ W_dq[N, K]^T (+ bias): replaces F.linear at quant/int_linear.py:62 for the
 // prefill / PPL-window shapes (M = 2048 per window, main.py:127-136; M = 65,536 for batch 32).
 //
-// v1 structure (one 256-thread block = 4 waves in a 2x2 grid, block tile 128(M) x 128(N), BK = 64):
-//   - A = x tile [128][64] fp16 and B = W tile [128][64] fp16 live in LDS with the 16-byte piece
-//     index XOR-swizzled by (row & 7) so a 32-row fragment read spreads over the bank row;
-//   - each thread owns one 32-code lane chunk of the W tile: it loads bits*4 bytes of packed codes
-//     and one (scale, zero), dequantizes bit-exactly (qlin_common.h) and writes 64 bytes of fp16;
+// v1 structure (one 256-thread block = 4 waves in a 2x2 grid, block tile 128(M) x 128(N), BK = 128
+// = one k-tile of the packed layout):
+//   - A = x tile [128][128] fp16 and B = W tile [128][128] fp16 live in LDS with the 16-byte piece
+//     index XOR-swizzled by (row & 15) so a 32-row fragment read is bank-conflict-free;
+//   - each thread stages two lane pieces of the 8 packed row tiles (coalesced 1 KB per wave),
+//     dequantizes them bit-exactly (qlin_common.h) and writes 4 x 16 B of fp16 per piece;
 //   - the next K-step's global loads are issued before this step's MFMAs (register prefetch);
 //   - each wave computes a 64x64 sub-tile as 2x2 v_mfma_f32_32x32x16_f16 accumulators.
 #include "qlin_common.h"
@@ -18,91 +19,92 @@ using namespace qlin;
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
+constexpr int BM = 128, BN = 128, BK = kTileK;  // one k-tile of the packed layout per K-step
+constexpr int kRowBytes = BK * 2;                 // 256 B per LDS row = one LDS bank row
 
-__device__ __forceinline__ int swz(int row, int piece) {  // byte offset of 16-B piece in a tile
-  return row * kRowBytes + 16 * (piece ^ (row & 7));
-}
+// byte offset of 16-B piece c (0..15) of LDS row r: piece index XOR (r & 15) spreads the 16 rows
+// read by a ds_read_b128 lane group over all 16 bank slots (conflict-free)
+__device__ __forceinline__ int swz(int r, int c) { return r * kRowBytes + 16 * (c ^ (r & 15)); }
 
-template <int BITS, bool WIDE>
+// the two lane pieces a thread stages per K-step: pieces tid and tid + 256 of the 8 row tiles
+template <int BITS, int GPT>
 struct BStage {
-  Chunk<BITS> c;
-  _Float16 s;
-  int z;
+  Piece<BITS> c[2];
+  uint32_t sz[2][GPT];  // packed (scale, zero) words, decoded at use
 };
 
-template <int BITS, bool WIDE>
-__device__ __forceinline__ void load_b(BStage<BITS, WIDE>& b, const uint32_t* __restrict__ qw,
-                                       const _Float16* __restrict__ scales,
-                                       const void* __restrict__ zeros, int64_t n, int N, int k0,
-                                       int K, int group, int tid) {
-  // tile row = tid / 2, chunk within BK = tid & 1
-  const int r = tid >> 1;
-  const int kc = (k0 >> 5) + (tid & 1);
-  const int64_t row = min(n + r, (int64_t)N - 1);
-  const int nch = K >> 5;
-  b.c = load_chunk<BITS>(qw + (row * nch + kc) * BITS);
-  const int64_t gi = row * (K / group) + (kc * 32) / group;
-  b.s = scales[gi];
-  if constexpr (WIDE) b.z = ((const int16_t*)zeros)[gi];
-  else b.z = ((const int8_t*)zeros)[gi];
+template <int BITS, int GPT>
+__device__ __forceinline__ void load_b(BStage<BITS, GPT>& b, const uint32_t* __restrict__ qw,
+                                       const uint32_t* __restrict__ qsz, int64_t nt0, int kt,
+                                       int Kt, int N, int K, int group, int tid) {
+  const int G = K / group;
+  const int64_t ntl = (N + kTileN - 1) / kTileN - 1;  // last row tile that exists
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int p = tid + kThreads * h;
+    const int rt = p >> 6, lane = p & 63;
+    const int64_t nt = min(nt0 + rt, ntl);
+    b.c[h] = load_piece<BITS>(qw + piece_off(nt, kt, Kt, lane, BITS));
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) {
+      const int g = min((kt * kTileK + 32 * (i * 4 / GPT)) / group, G - 1);
+      b.sz[h][i] = qsz[sz_index(nt, g, G, lane & 15)];
+    }
+  }
 }
 
-__device__ __forceinline__ void load_a(uint4 (&a)[4], const _Float16* __restrict__ x, int64_t m0,
+template <int BITS, int GPT, bool WIDE>
+__device__ __forceinline__ void store_b(unsigned char* sB, const BStage<BITS, GPT>& b, int kt,
+                                        int K, int tid) {
+  const Magics mg = make_magics<BITS>();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int p = tid + kThreads * h;
+    const int rt = p >> 6, lane = p & 63;
+    const int r = rt * kTileN + (lane & 15), q = lane >> 4;
+    auto one = [&](auto S_) {
+      constexpr int S = decltype(S_)::value;
+      uint32_t o[4] = {0u, 0u, 0u, 0u};
+      if (kt * kTileK + 32 * S < K) {
+        constexpr int slot = S * GPT / 4;
+        const GroupQ g = make_group<BITS, WIDE>(sz_scale(b.sz[h][slot]), sz_zero(b.sz[h][slot]));
+        dequant_step<BITS, WIDE, S>(b.c[h], mg, g, o);
+      }
+      *reinterpret_cast<uint4*>(sB + swz(r, 4 * S + q)) = make_uint4(o[0], o[1], o[2], o[3]);
+    };
+    one(std::integral_constant<int, 0>{});
+    one(std::integral_constant<int, 1>{});
+    one(std::integral_constant<int, 2>{});
+    one(std::integral_constant<int, 3>{});
+  }
+}
+
+// x tile [128 rows][128 k]: 2048 16-B pieces, 8 per thread; k >= K and m >= M read as zero
+__device__ __forceinline__ void load_a(uint4 (&a)[8], const _Float16* __restrict__ x, int64_t m0,
                                        int64_t M, int k0, int K, int tid) {
-  // 128 rows x 8 pieces = 1024 pieces; thread handles pieces tid + 256*i
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 8; ++i) {
     const int p = tid + kThreads * i;
-    const int r = p >> 3, pc = p & 7;
+    const int r = p >> 4, c = p & 15;
     const int64_t m = m0 + r;
-    a[i] = m < M ? *reinterpret_cast<const uint4*>(x + m * K + k0 + pc * 8) : make_uint4(0, 0, 0, 0);
+    const int k = k0 + 8 * c;
+    a[i] = (m < M && k < K) ? *reinterpret_cast<const uint4*>(x + m * K + k) : make_uint4(0, 0, 0, 0);
   }
 }
 
-template <int BITS, bool WIDE>
-__device__ __forceinline__ void store_b(unsigned char* sB, const BStage<BITS, WIDE>& b, int tid) {
-  const GroupQ g = make_group<WIDE>(b.s, b.z);
-  const int r = tid >> 1;
-  const int pbase = (tid & 1) * 4;  // 4 pieces of 8 halfs
-  uint32_t o[16];
-  o[0] = as_u32(dequant_pair<BITS, WIDE, 0>(b.c, g));
-  o[1] = as_u32(dequant_pair<BITS, WIDE, 1>(b.c, g));
-  o[2] = as_u32(dequant_pair<BITS, WIDE, 2>(b.c, g));
-  o[3] = as_u32(dequant_pair<BITS, WIDE, 3>(b.c, g));
-  o[4] = as_u32(dequant_pair<BITS, WIDE, 4>(b.c, g));
-  o[5] = as_u32(dequant_pair<BITS, WIDE, 5>(b.c, g));
-  o[6] = as_u32(dequant_pair<BITS, WIDE, 6>(b.c, g));
-  o[7] = as_u32(dequant_pair<BITS, WIDE, 7>(b.c, g));
-  o[8] = as_u32(dequant_pair<BITS, WIDE, 8>(b.c, g));
-  o[9] = as_u32(dequant_pair<BITS, WIDE, 9>(b.c, g));
-  o[10] = as_u32(dequant_pair<BITS, WIDE, 10>(b.c, g));
-  o[11] = as_u32(dequant_pair<BITS, WIDE, 11>(b.c, g));
-  o[12] = as_u32(dequant_pair<BITS, WIDE, 12>(b.c, g));
-  o[13] = as_u32(dequant_pair<BITS, WIDE, 13>(b.c, g));
-  o[14] = as_u32(dequant_pair<BITS, WIDE, 14>(b.c, g));
-  o[15] = as_u32(dequant_pair<BITS, WIDE, 15>(b.c, g));
+__device__ __forceinline__ void store_a(unsigned char* sA, const uint4 (&a)[8], int tid) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    *reinterpret_cast<uint4*>(sB + swz(r, pbase + i)) =
-        make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
-}
-
-__device__ __forceinline__ void store_a(unsigned char* sA, const uint4 (&a)[4], int tid) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 8; ++i) {
     const int p = tid + kThreads * i;
-    *reinterpret_cast<uint4*>(sA + swz(p >> 3, p & 7)) = a[i];
+    *reinterpret_cast<uint4*>(sA + swz(p >> 4, p & 15)) = a[i];
   }
 }
 
-template <int BITS, bool WIDE>
+template <int BITS, int GPT, bool WIDE>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(
-    const uint32_t* __restrict__ qw, const _Float16* __restrict__ scales,
-    const void* __restrict__ zeros, const _Float16* __restrict__ x,
-    const _Float16* __restrict__ bias, _Float16* __restrict__ y, int64_t M, int N, int K,
-    int group, int tiles_n) {
+    const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
+    const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
+    int64_t M, int N, int K, int group, int tiles_n) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BM * kRowBytes];
   unsigned char* sA = smem;
   unsigned char* sB = smem + BM * kRowBytes;
@@ -110,11 +112,12 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  // n-tile fastest: consecutive blocks share the x tile
+  // n-tile fastest: consecutive blocks share the x tile in L2
   const int64_t tile_m = blockIdx.x / tiles_n;
   const int tile_n = blockIdx.x - (int)(tile_m * tiles_n);
   const int64_t m0 = tile_m * BM;
-  const int64_t n0 = (int64_t)tile_n * BN;
+  const int64_t nt0 = (int64_t)tile_n * (BN / kTileN);
+  const int Kt = (K + kTileK - 1) / kTileK;
 
   f16v acc[2][2];
 #pragma unroll
@@ -124,31 +127,28 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  uint4 a[4];
-  BStage<BITS, WIDE> b;
+  uint4 a[8];
+  BStage<BITS, GPT> b;
   load_a(a, x, m0, M, 0, K, tid);
-  load_b<BITS, WIDE>(b, qw, scales, zeros, n0, N, 0, K, group, tid);
+  load_b<BITS, GPT>(b, qw, qsz, nt0, 0, Kt, N, K, group, tid);
 
-  const int nk = K / BK;
   const int r32 = lane & 31, h = lane >> 5;
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = 0; kt < Kt; ++kt) {
     __syncthreads();
     store_a(sA, a, tid);
-    store_b<BITS, WIDE>(sB, b, tid);
+    store_b<BITS, GPT, WIDE>(sB, b, kt, K, tid);
     __syncthreads();
-    if (kt + 1 < nk) {
+    if (kt + 1 < Kt) {
       load_a(a, x, m0, M, (kt + 1) * BK, K, tid);
-      load_b<BITS, WIDE>(b, qw, scales, zeros, n0, N, (kt + 1) * BK, K, group, tid);
+      load_b<BITS, GPT>(b, qw, qsz, nt0, kt + 1, Kt, N, K, group, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       h8 af[2], bf[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int ra = wm * 64 + i * 32 + r32;
-        af[i] = *reinterpret_cast<const h8*>(sA + swz(ra, kk * 2 + h));
-        const int rb = wn * 64 + i * 32 + r32;
-        bf[i] = *reinterpret_cast<const h8*>(sB + swz(rb, kk * 2 + h));
+        af[i] = *reinterpret_cast<const h8*>(sA + swz(wm * 64 + i * 32 + r32, kk * 2 + h));
+        bf[i] = *reinterpret_cast<const h8*>(sB + swz(wn * 64 + i * 32 + r32, kk * 2 + h));
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(
   // epilogue: C/D layout col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int64_t n = n0 + wn * 64 + j * 32 + r32;
+    const int64_t n = nt0 * kTileN + wn * 64 + j * 32 + r32;
     if (n >= N) continue;
     const float bv = bias ? (float)bias[n] : 0.f;
 #pragma unroll
@@ -175,42 +175,48 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(
   }
 }
 
-template <int BITS, bool WIDE>
-int launch_gemm(const uint32_t* qw, const uint16_t* sc, const void* z, const uint16_t* x,
-                const uint16_t* bias, uint16_t* y, int64_t M, int N, int K, int group,
-                hipStream_t st) {
+template <int BITS, int GPT, bool WIDE>
+int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
+                uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
   const int tiles_n = (N + BN - 1) / BN;
   const int64_t tiles_m = (M + BM - 1) / BM;
   const int64_t blocks = tiles_m * tiles_n;
   if (blocks > 0x7fffffff) return QLIN_EINVAL;
-  hipLaunchKernelGGL((gemm_kernel<BITS, WIDE>), dim3((unsigned)blocks), dim3(kThreads), 0, st, qw,
-                     (const _Float16*)sc, z, (const _Float16*)x, (const _Float16*)bias,
-                     (_Float16*)y, M, N, K, group, tiles_n);
+  hipLaunchKernelGGL((gemm_kernel<BITS, GPT, WIDE>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
+                     qw, qsz, (const _Float16*)x, (const _Float16*)bias, (_Float16*)y, M, N, K,
+                     group, tiles_n);
   return (int)hipGetLastError();
 }
 
-bool valid(int64_t M, int64_t N, int64_t K, int bits, int group, int zero_bits) {
-  return M >= 0 && N >= 0 && N <= (1 << 30) && K > 0 && K % BK == 0 && K <= (1 << 20) &&
+template <int BITS, bool WIDE>
+int launch_gemm_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
+                  uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
+  if (group % 128 == 0) return launch_gemm<BITS, 1, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (group % 64 == 0) return launch_gemm<BITS, 2, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  return launch_gemm<BITS, 4, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+}
+
+bool valid(int64_t M, int64_t N, int64_t K, int bits, int group) {
+  return M >= 0 && N >= 0 && N <= (1 << 30) && K > 0 && K % 32 == 0 && K <= (1 << 20) &&
          group > 0 && group % 32 == 0 && K % group == 0 &&
-         (bits == 2 || bits == 3 || bits == 4 || bits == 8) && (zero_bits == 8 || zero_bits == 16);
+         (bits == 2 || bits == 3 || bits == 4 || bits == 8);
 }
 
 }  // namespace
 
-extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
-                             int zero_bits, const uint16_t* x, const uint16_t* bias, uint16_t* y,
-                             int64_t M, int64_t N, int64_t K, int bits, int group,
-                             void* workspace, void* stream) {
+extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                             const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
+                             int64_t N, int64_t K, int bits, int group, void* workspace,
+                             void* stream) {
   (void)workspace;
-  if (!qweight || !scales || !zeros || !x || !y || !valid(M, N, K, bits, group, zero_bits))
-    return QLIN_EINVAL;
+  if (!qweight || !qsz || !x || !y || !valid(M, N, K, bits, group)) return QLIN_EINVAL;
   if (M == 0 || N == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
-  const bool wide = zero_bits == 16;
+  const bool wide = flags & QLIN_WIDE_ZERO;
   const int n = (int)N, k = (int)K;
-#define QLIN_M(B)                                                                            \
-  return wide ? launch_gemm<B, true>(qweight, scales, zeros, x, bias, y, M, n, k, group, st) \
-              : launch_gemm<B, false>(qweight, scales, zeros, x, bias, y, M, n, k, group, st)
+#define QLIN_M(B)                                                                     \
+  return wide ? launch_gemm_g<B, true>(qweight, qsz, x, bias, y, M, n, k, group, st) \
+              : launch_gemm_g<B, false>(qweight, qsz, x, bias, y, M, n, k, group, st)
   switch (bits) {
     case 2: QLIN_M(2);
     case 3: QLIN_M(3);
@@ -220,13 +226,10 @@ extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint16_t* scales, co
 #undef QLIN_M
 }
 
-extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint16_t* scales, const void* zeros,
-                               int zero_bits, const uint16_t* x, const uint16_t* bias,
-                               uint16_t* y, int64_t M, int64_t N, int64_t K, int bits, int group,
-                               void* stream) {
-  if (M <= 4 && K <= 16384)
-    return qlin_gemv_f16(qweight, scales, zeros, zero_bits, x, bias, y, M, N, K, bits, group,
-                         stream);
-  return qlin_gemm_f16(qweight, scales, zeros, zero_bits, x, bias, y, M, N, K, bits, group,
-                       nullptr, stream);
+extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                               const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
+                               int64_t N, int64_t K, int bits, int group, void* stream) {
+  if (M == 0) return QLIN_OK;
+  if (M <= 4) return qlin_gemv_f16(qweight, qsz, flags, x, bias, y, M, N, K, bits, group, stream);
+  return qlin_gemm_f16(qweight, qsz, flags, x, bias, y, M, N, K, bits, group, nullptr, stream);
 }

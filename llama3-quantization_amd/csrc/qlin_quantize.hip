@@ -6,10 +6,11 @@
 // (:146-159), then fake_quant (:94-115) — every op rounded to the element dtype exactly as the
 // reference's fp16/fp32 torch ops round (oracle/quant_oracle.py restates the same arithmetic).
 //
-// Work decomposition: a block of 256 threads owns RPB whole rows; a thread owns 32-element lane
-// chunks (the packing granule).  Phase 1 reduces each chunk's min/max into LDS; phase 2 reduces
-// one group per thread (a group never crosses a row) and computes (scale, zp); phase 3 re-reads
-// the chunk (L2-hot), fake-quantizes it and writes x_dq and/or the packed words.
+// Work decomposition: a block of 256 threads owns RPB whole rows.  Phase 1 reduces the min/max of
+// each 32-element chunk into LDS; phase 2 reduces one group per thread (a group never crosses a
+// row) and computes (scale, zp); phase 3 walks the rows' lane pieces (qlin_common.h tiled layout:
+// 4 x 8 elements of one row), re-reads them (L2-hot), fake-quantizes, and writes x_dq and/or the
+// packed piece.
 #include "qlin_common.h"
 #include "../../include/qlin_gfx950.h"
 
@@ -44,54 +45,57 @@ __device__ __forceinline__ void load32(const T* __restrict__ p, float (&v)[32]) 
   }
 }
 
+// 8 consecutive elements <-> float
 template <typename T>
-__device__ __forceinline__ void store32(T* __restrict__ p, const float (&v)[32]) {
+__device__ __forceinline__ void load8(const T* __restrict__ p, float* v) {
   if constexpr (sizeof(T) == 2) {
+    const h8 h = *reinterpret_cast<const h8*>(p);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      h8 h;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[8 * i + j];
-      *reinterpret_cast<h8*>(p + 8 * i) = h;
-    }
+    for (int j = 0; j < 8; ++j) v[j] = (float)h[j];
   } else {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* __restrict__ p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    h8 h;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      *reinterpret_cast<float4*>(p + 4 * i) = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+    for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[j];
+    *reinterpret_cast<h8*>(p) = h;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
 }
 
-// pack 32 unsigned codes (as floats holding exact small integers) into BITS words
+// pack the 32 codes u[8s + j] of one lane piece (step s, element j) — qlin_common.h layout
 template <int BITS>
-__device__ __forceinline__ void pack_chunk(const uint32_t (&u)[32], uint32_t* __restrict__ out) {
-  if constexpr (BITS == 2 || BITS == 4 || BITS == 8) {
-    constexpr int P = 16 / BITS;
+__device__ __forceinline__ void pack_piece(const uint32_t (&u)[32], uint32_t* __restrict__ out) {
+  uint32_t w[BITS];
 #pragma unroll
-    for (int i = 0; i < BITS; ++i) {
-      uint32_t w = 0;
+  for (int i = 0; i < BITS; ++i) w[i] = 0;
 #pragma unroll
-      for (int p = 0; p < P; ++p) {
-        w |= u[i * 2 * P + 2 * p] << (BITS * p);
-        w |= u[i * 2 * P + 2 * p + 1] << (16 + BITS * p);
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t c = u[8 * s + j];
+      const int h = j & 1, p = j >> 1;
+      if constexpr (BITS == 4) {
+        w[s] |= c << (16 * h + 4 * p);
+      } else if constexpr (BITS == 8) {
+        w[2 * s + (j >> 2)] |= c << (16 * h + 8 * ((j & 3) >> 1));
+      } else {
+        w[s >> 1] |= (c & 3u) << (16 * h + 8 * (s & 1) + 2 * p);
+        if constexpr (BITS == 3)
+          w[2] |= ((c >> 2) & 1u) << ((16 * h + 2 * p + 2 + rho3(s)) & 31);
       }
-      out[i] = w;
     }
-  } else {  // 3: low two bits in the 2-bit layout, bit 2 in word 2
-    uint32_t w0 = 0, w1 = 0, w2 = 0;
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      w0 |= (u[2 * p] & 3u) << (2 * p);
-      w0 |= (u[2 * p + 1] & 3u) << (16 + 2 * p);
-      w1 |= (u[16 + 2 * p] & 3u) << (2 * p);
-      w1 |= (u[16 + 2 * p + 1] & 3u) << (16 + 2 * p);
-    }
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      w2 |= ((u[2 * p] >> 2) & 1u) << p;
-      w2 |= ((u[2 * p + 1] >> 2) & 1u) << (16 + p);
-    }
-    out[0] = w0; out[1] = w1; out[2] = w2;
   }
+#pragma unroll
+  for (int i = 0; i < BITS; ++i) out[i] = w[i];
 }
 
 // (scale, zp) of one group — quant/quantizer.py:141-159
@@ -139,7 +143,7 @@ template <typename T, int BITS>  // BITS == 0: no packed output
 __global__ __launch_bounds__(kThreads) void quantize_kernel(
     const T* __restrict__ x, QP P, const T* __restrict__ up, const T* __restrict__ low,
     T* __restrict__ x_dq, T* __restrict__ scale_out, T* __restrict__ zp_out,
-    uint32_t* __restrict__ qweight, _Float16* __restrict__ scales, int16_t* __restrict__ zeros16) {
+    uint32_t* __restrict__ qweight, uint32_t* __restrict__ qsz) {
   __shared__ float s_min[kMaxChunks];
   __shared__ float s_max[kMaxChunks];
   __shared__ float s_scale[kMaxChunks];
@@ -181,32 +185,47 @@ __global__ __launch_bounds__(kThreads) void quantize_kernel(
     if (scale_out) scale_out[g0 + gi] = (T)scale;
     if (zp_out && has_zp) zp_out[g0 + gi] = (T)zp;
     if constexpr (BITS > 0) {
-      scales[g0 + gi] = (_Float16)scale;
-      zeros16[g0 + gi] = has_zp ? (int16_t)zp : (int16_t)(1 << (BITS - 1));
+      const int Gr = P.K / P.group;
+      const int64_t row = row0 + gi / Gr;
+      const int g = gi - (gi / Gr) * Gr;
+      qsz[sz_index(row >> 4, g, Gr, (int)(row & 15))] =
+          sz_pack((_Float16)scale, has_zp ? (int)zp : (1 << (BITS - 1)));
     }
   }
   __syncthreads();
 
-  // phase 3: fake-quant (+ pack)
-  for (int c = tid; c < nch; c += kThreads) {
-    float v[32];
-    load32<T>(xb + (int64_t)c * 32, v);
-    const int gi = c / P.cpg;
-    const float s = s_scale[gi], zp = s_zp[gi];
-    float o[32];
+  // phase 3: fake-quant (+ pack), one lane piece (row, k-tile, q) per thread iteration
+  const int Kt = (P.K + kTileK - 1) / kTileK;
+  const int npc = nrows * Kt * 4;
+  for (int pc = tid; pc < npc; pc += kThreads) {
+    const int r = pc / (Kt * 4);
+    const int rem = pc - r * Kt * 4;
+    const int kt = rem >> 2, q = rem & 3;
+    const int64_t row = row0 + r;
     uint32_t u[32];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      float xi;
-      o[i] = fq<T>(v[i], s, zp, has_zp, P, xi);
-      if (!has_zp) xi += (float)(1 << (P.bits - 1));
-      u[i] = (xi == xi) ? (uint32_t)(int)xi : 0u;  // NaN (x/s overflow) has no code: 0
+    for (int st = 0; st < 4; ++st) {
+      const int k0 = kt * kTileK + 32 * st + 8 * q;
+      if (k0 < P.K) {
+        float v[8], o[8];
+        load8<T>(x + row * P.K + k0, v);
+        const int gi = r * (P.K / P.group) + k0 / P.group;
+        const float sc = s_scale[gi], zp = s_zp[gi];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float xi;
+          o[j] = fq<T>(v[j], sc, zp, has_zp, P, xi);
+          if (!has_zp) xi += (float)(1 << (P.bits - 1));
+          u[8 * st + j] = (xi == xi) ? (uint32_t)(int)xi : 0u;  // NaN (x/s overflow): code 0
+        }
+        if (x_dq) store8<T>(x_dq + row * P.K + k0, o);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[8 * st + j] = 0u;
+      }
     }
-    if (x_dq) store32<T>(x_dq + row0 * P.K + (int64_t)c * 32, o);
-    if constexpr (BITS > 0) {
-      const int r = c / P.cpr, cc = c - r * P.cpr;
-      pack_chunk<BITS>(u, qweight + (row0 + r) * (int64_t)(P.cpr * BITS) + (int64_t)cc * BITS);
-    }
+    if constexpr (BITS > 0)
+      pack_piece<BITS>(u, qweight + piece_off(row >> 4, kt, Kt, (int)(row & 15) + 16 * q, BITS));
   }
 }
 
@@ -216,46 +235,55 @@ __global__ __launch_bounds__(kThreads) void quantize_kernel(
 template <typename T, int BITS>  // BITS == 0: no packed output
 __global__ __launch_bounds__(kThreads) void fq_kernel(
     const T* __restrict__ x, const T* __restrict__ sref, const T* __restrict__ zref,
-    int64_t total_chunks, int K, int group, int bits, int flags, T* __restrict__ x_dq,
-    uint32_t* __restrict__ qweight, _Float16* __restrict__ scales, int16_t* __restrict__ zeros16) {
-  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (c >= total_chunks) return;
-  const int cpr = K / 32;
-  const int64_t row = c / cpr;
-  const int cc = (int)(c - row * cpr);
-  const int64_t gidx = row * (K / group) + (int64_t)cc * 32 / group;
+    int64_t total_pieces, int K, int group, int bits, int flags, T* __restrict__ x_dq,
+    uint32_t* __restrict__ qweight, uint32_t* __restrict__ qsz) {
+  const int64_t pc = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (pc >= total_pieces) return;
+  const int Kt = (K + kTileK - 1) / kTileK;
+  const int64_t row = pc / (Kt * 4);
+  const int rem = (int)(pc - row * Kt * 4);
+  const int kt = rem >> 2, q = rem & 3;
   const bool has_zp = !(flags & QLIN_DISABLE_ZERO_POINT);
   QP P;
   P.bits = bits;
   P.qmin = has_zp ? 0.f : -(float)(1 << (bits - 1));
   P.qmax = has_zp ? (float)((1 << bits) - 1) : (float)((1 << (bits - 1)) - 1);
-  const float s = (float)sref[gidx];
-  const float zp = has_zp ? (float)zref[gidx] : 0.f;
-  float v[32];
-  load32<T>(x + c * 32, v);
-  float o[32];
   uint32_t u[32];
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    float xi;
-    o[i] = fq<T>(v[i], s, zp, has_zp, P, xi);
-    if (!has_zp) xi += (float)(1 << (bits - 1));
-    u[i] = (xi == xi) ? (uint32_t)(int)xi : 0u;
-  }
-  if (x_dq) store32<T>(x_dq + c * 32, o);
-  if constexpr (BITS > 0) {
-    pack_chunk<BITS>(u, qweight + c * BITS);
-    if ((cc * 32) % group == 0) {
-      scales[gidx] = (_Float16)s;
-      zeros16[gidx] = has_zp ? (int16_t)zp : (int16_t)(1 << (BITS - 1));
+  for (int st = 0; st < 4; ++st) {
+    const int k0 = kt * kTileK + 32 * st + 8 * q;
+    if (k0 < K) {
+      const int64_t gidx = row * (K / group) + k0 / group;
+      const float sc = (float)sref[gidx];
+      const float zp = has_zp ? (float)zref[gidx] : 0.f;
+      float v[8], o[8];
+      load8<T>(x + row * K + k0, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float xi;
+        o[j] = fq<T>(v[j], sc, zp, has_zp, P, xi);
+        if (!has_zp) xi += (float)(1 << (bits - 1));
+        u[8 * st + j] = (xi == xi) ? (uint32_t)(int)xi : 0u;
+      }
+      if (x_dq) store8<T>(x_dq + row * K + k0, o);
+      if constexpr (BITS > 0) {
+        if (k0 % group == 0)
+          qsz[sz_index(row >> 4, k0 / group, K / group, (int)(row & 15))] =
+              sz_pack((_Float16)sc, has_zp ? (int)zp : (1 << (BITS - 1)));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[8 * st + j] = 0u;
     }
   }
+  if constexpr (BITS > 0)
+    pack_piece<BITS>(u, qweight + piece_off(row >> 4, kt, Kt, (int)(row & 15) + 16 * q, BITS));
 }
 
 template <typename T>
 int launch_quantize(const void* x, int64_t rows, int64_t K, int bits, int group, int flags,
                     const void* up, const void* low, void* x_dq, void* scale_out, void* zp_out,
-                    uint32_t* qweight, uint16_t* scales, int16_t* zeros16, hipStream_t st) {
+                    uint32_t* qweight, uint32_t* qsz, hipStream_t st) {
   QP P;
   P.rows = rows;
   P.K = (int)K;
@@ -274,7 +302,7 @@ int launch_quantize(const void* x, int64_t rows, int64_t K, int bits, int group,
 #define QLIN_Q(B)                                                                            \
   hipLaunchKernelGGL((quantize_kernel<T, B>), grid, dim3(kThreads), 0, st, xx, P,            \
                      (const T*)up, (const T*)low, (T*)x_dq, (T*)scale_out, (T*)zp_out,       \
-                     qweight, (_Float16*)scales, zeros16)
+                     qweight, qsz)
   if (!pack) QLIN_Q(0);
   else if (bits == 2) QLIN_Q(2);
   else if (bits == 3) QLIN_Q(3);
@@ -297,51 +325,49 @@ extern "C" const char* qlin_error_string(int code) {
 extern "C" int qlin_quantize(const void* x, int dtype, int64_t rows, int64_t K, int bits,
                              int group, int flags, const void* lwc_up_sig,
                              const void* lwc_low_sig, void* x_dq, void* scale_out, void* zp_out,
-                             uint32_t* qweight, uint16_t* scales, int16_t* zeros16,
-                             void* stream) {
+                             uint32_t* qweight, uint32_t* qsz, void* stream) {
   if (!x || rows < 0 || K <= 0 || K % 32 || K / 32 > kMaxChunks || group <= 0 || group % 32 ||
       K % group || bits < 2 || bits > 8 || (dtype != QLIN_F16 && dtype != QLIN_F32))
     return QLIN_EINVAL;
   if ((flags & QLIN_LWC) && (!lwc_up_sig || !lwc_low_sig)) return QLIN_EINVAL;
-  const bool pack = qweight || scales || zeros16;
-  if (pack && (!qweight || !scales || !zeros16 || dtype != QLIN_F16 ||
+  const bool pack = qweight || qsz;
+  if (pack && (!qweight || !qsz || dtype != QLIN_F16 ||
                !(bits == 2 || bits == 3 || bits == 4 || bits == 8)))
     return QLIN_EINVAL;
   if (rows == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == QLIN_F16)
     return launch_quantize<_Float16>(x, rows, K, bits, group, flags, lwc_up_sig, lwc_low_sig,
-                                     x_dq, scale_out, zp_out, qweight, scales, zeros16, st);
+                                     x_dq, scale_out, zp_out, qweight, qsz, st);
   return launch_quantize<float>(x, rows, K, bits, group, flags, lwc_up_sig, lwc_low_sig, x_dq,
-                                scale_out, zp_out, nullptr, nullptr, nullptr, st);
+                                scale_out, zp_out, nullptr, nullptr, st);
 }
 
 extern "C" int qlin_fake_quant(const void* x, int dtype, const void* scale, const void* zp,
                                int64_t rows, int64_t K, int bits, int group, int flags,
-                               void* x_dq, uint32_t* qweight, uint16_t* scales, int16_t* zeros16,
-                               void* stream) {
+                               void* x_dq, uint32_t* qweight, uint32_t* qsz, void* stream) {
   const bool has_zp = !(flags & QLIN_DISABLE_ZERO_POINT);
-  const bool pack = qweight || scales || zeros16;
+  const bool pack = qweight || qsz;
   if (!x || !scale || (has_zp && !zp) || rows < 0 || K <= 0 || K % 32 || group <= 0 ||
       group % 32 || K % group || bits < 2 || bits > 8 || (dtype != QLIN_F16 && dtype != QLIN_F32))
     return QLIN_EINVAL;
-  if (pack && (!qweight || !scales || !zeros16 || dtype != QLIN_F16 ||
+  if (pack && (!qweight || !qsz || dtype != QLIN_F16 ||
                !(bits == 2 || bits == 3 || bits == 4 || bits == 8)))
     return QLIN_EINVAL;
-  const int64_t chunks = rows * (K / 32);
-  if (chunks == 0) return QLIN_OK;
+  const int64_t pieces = rows * ((K + kTileK - 1) / kTileK) * 4;
+  if (pieces == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((unsigned)((chunks + kThreads - 1) / kThreads));
+  const dim3 grid((unsigned)((pieces + kThreads - 1) / kThreads));
   if (dtype == QLIN_F32) {
     hipLaunchKernelGGL((fq_kernel<float, 0>), grid, dim3(kThreads), 0, st, (const float*)x,
-                       (const float*)scale, (const float*)zp, chunks, (int)K, group, bits, flags,
-                       (float*)x_dq, nullptr, nullptr, nullptr);
+                       (const float*)scale, (const float*)zp, pieces, (int)K, group, bits, flags,
+                       (float*)x_dq, nullptr, nullptr);
     return (int)hipGetLastError();
   }
 #define QLIN_P(B)                                                                            \
   hipLaunchKernelGGL((fq_kernel<_Float16, B>), grid, dim3(kThreads), 0, st, (const _Float16*)x, \
-                     (const _Float16*)scale, (const _Float16*)zp, chunks, (int)K, group, bits,  \
-                     flags, (_Float16*)x_dq, qweight, (_Float16*)scales, zeros16)
+                     (const _Float16*)scale, (const _Float16*)zp, pieces, (int)K, group, bits,  \
+                     flags, (_Float16*)x_dq, qweight, qsz)
   if (!pack) QLIN_P(0);
   else if (bits == 2) QLIN_P(2);
   else if (bits == 3) QLIN_P(3);
@@ -353,9 +379,8 @@ extern "C" int qlin_fake_quant(const void* x, int dtype, const void* scale, cons
 
 extern "C" int qlin_pack_f16(const uint16_t* w_dq, const uint16_t* scales_ref,
                              const uint16_t* zeros_ref, int64_t N, int64_t K, int bits, int group,
-                             int flags, uint32_t* qweight, uint16_t* scales, int16_t* zeros16,
-                             void* stream) {
-  if (!w_dq || !qweight || !scales || !zeros16) return QLIN_EINVAL;
+                             int flags, uint32_t* qweight, uint32_t* qsz, void* stream) {
+  if (!w_dq || !qweight || !qsz) return QLIN_EINVAL;
   return qlin_fake_quant(w_dq, QLIN_F16, scales_ref, zeros_ref, N, K, bits, group, flags, nullptr,
-                         qweight, scales, zeros16, stream);
+                         qweight, qsz, stream);
 }

@@ -12,7 +12,7 @@ Added (the real-quant path of quant/omniquant.py:315-335, re-done for MI355X):
     canonical gfx950 layout (``qlin_pack_f16``) and switches ``fwd_func`` to the fused
     unpack + dequant + GEMV/MFMA-GEMM kernels (``qlin_linear_f16``).  ``pack_from_weight()`` does the
     RTN quantize + pack of a float weight in one kernel.
-  * ``packed`` / ``qweight`` / ``qscales`` / ``qzeros`` / ``wbits`` / ``group`` state.
+  * ``packed`` / ``qweight`` / ``qsz`` / ``qflags`` / ``wbits`` / ``group`` state.
 """
 import torch
 import torch.nn as nn
@@ -58,6 +58,7 @@ class QuantLinear(nn.Module):
         self.packed = False
         self.wbits = None
         self.group = None
+        self.qflags = 0
 
     def forward(self, input: torch.Tensor):
         if self.packed:
@@ -90,15 +91,15 @@ class QuantLinear(nn.Module):
         x = input
         if x.dtype != torch.float16:
             x = x.to(torch.float16)
-        y = qlin.linear(x.contiguous(), self.qweight, self.qscales, self.qzeros,
+        y = qlin.linear(x.contiguous(), self.qweight, self.qsz,
                         None if bias is None else bias.to(torch.float16).contiguous(),
-                        self.out_features, self.in_features, self.wbits, self.group)
+                        self.out_features, self.in_features, self.wbits, self.group, self.qflags)
         return y if input.dtype == torch.float16 else y.to(input.dtype)
 
-    def _install(self, qweight, scales, zeros, bits, group, keep_weight):
-        self.register_buffer("qweight", qweight)
-        self.register_buffer("qscales", scales)
-        self.register_buffer("qzeros", qlin.narrow_zeros(zeros))
+    def _install(self, out, bits, group, keep_weight):
+        self.register_buffer("qweight", out["qweight"])
+        self.register_buffer("qsz", out["qsz"])
+        self.qflags = out["flags"]
         self.wbits = bits
         self.group = group
         self.packed = True
@@ -130,7 +131,7 @@ class QuantLinear(nn.Module):
         z = None if wq.zeros is None else wq.zeros.to(torch.float16).reshape(-1).contiguous()
         flags = qlin.DISABLE_ZERO_POINT if z is None else 0
         out = qlin.fake_quant(w, s, z, wq.n_bits, group, flags, want_xdq=False, pack=True)
-        self._install(out["qweight"], out["scales"], out["zeros"], wq.n_bits, group, keep_weight)
+        self._install(out, wq.n_bits, group, keep_weight)
         return self
 
     @torch.no_grad()
@@ -143,7 +144,7 @@ class QuantLinear(nn.Module):
         w = self.weight.to(torch.float16).contiguous()
         out = qlin.quantize(w, wq.n_bits, group, wq._flags(), want_xdq=keep_weight,
                             want_params=False, pack=True)
-        self._install(out["qweight"], out["scales"], out["zeros"], wq.n_bits, group, keep_weight)
+        self._install(out, wq.n_bits, group, keep_weight)
         if keep_weight:
             self.weight = out["x_dq"]
         return self
@@ -152,8 +153,8 @@ class QuantLinear(nn.Module):
         """W_dq [out, in] fp16 from the packed codes (bit-exact)."""
         if not self.packed:
             raise RuntimeError("module is not packed")
-        return qlin.dequant(self.qweight, self.qscales, self.qzeros, self.out_features,
-                            self.in_features, self.wbits, self.group)
+        return qlin.dequant(self.qweight, self.qsz, self.out_features, self.in_features,
+                            self.wbits, self.group, self.qflags)
 
     def extra_repr(self):
         s = f"in_features={self.in_features}, out_features={self.out_features}"

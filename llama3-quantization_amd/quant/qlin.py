@@ -16,11 +16,12 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
 LWC = 4
+WIDE_ZERO = 8
 F16 = 0
 F32 = 1
 
@@ -36,13 +37,13 @@ _l = ctypes.c_int64
 SIGNATURES = {
     "qlin_abi_version": ([], _i),
     "qlin_error_string": ([_i], ctypes.c_char_p),
-    "qlin_quantize": ([_p, _i, _l, _l, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p], _i),
-    "qlin_fake_quant": ([_p, _i, _p, _p, _l, _l, _i, _i, _i, _p, _p, _p, _p, _p], _i),
-    "qlin_pack_f16": ([_p, _p, _p, _l, _l, _i, _i, _i, _p, _p, _p, _p], _i),
-    "qlin_dequant_f16": ([_p, _p, _p, _i, _l, _l, _i, _i, _p, _p], _i),
-    "qlin_gemv_f16": ([_p, _p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
-    "qlin_gemm_f16": ([_p, _p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
-    "qlin_linear_f16": ([_p, _p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
+    "qlin_quantize": ([_p, _i, _l, _l, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p], _i),
+    "qlin_fake_quant": ([_p, _i, _p, _p, _l, _l, _i, _i, _i, _p, _p, _p, _p], _i),
+    "qlin_pack_f16": ([_p, _p, _p, _l, _l, _i, _i, _i, _p, _p, _p], _i),
+    "qlin_dequant_f16": ([_p, _p, _i, _l, _l, _i, _i, _p, _p], _i),
+    "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
+    "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
+    "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
 }
 
 
@@ -106,12 +107,62 @@ def _dtcode(t):
     return _DT[t.dtype]
 
 
+TILE_N = 16
+TILE_K = 128
+
+
+def packed_shape(N: int, K: int, bits: int):
+    """qweight shape of the tiled layout: [ceil(N/16), ceil(K/128), 64 lanes, bits words]."""
+    return (-(-N // TILE_N), -(-K // TILE_K), 64, bits)
+
+
+def sz_shape(N: int, K: int, group: int):
+    """qsz shape: [ceil(N/16), K/group, 16] words of (fp16 scale | int16 zero << 16)."""
+    return (-(-N // TILE_N), K // group, TILE_N)
+
+
+WIDE_LIMIT = 1024  # |zero| above this needs the fp32 (u - zero) path (QLIN_WIDE_ZERO)
+
+
+def _alloc_packed(rows, K, bits, group, device):
+    qw = torch.zeros(packed_shape(rows, K, bits), dtype=torch.int32, device=device)
+    qsz = torch.zeros(sz_shape(rows, K, group), dtype=torch.int32, device=device)
+    return qw, qsz
+
+
+def split_sz(qsz: torch.Tensor, N: int):
+    """qsz -> (scales fp16 [N, G], zeros int16 [N, G]) — the reference's scales / zeros views."""
+    nt, G, _ = qsz.shape
+    w = qsz.permute(0, 2, 1).reshape(nt * TILE_N, G)[:N]
+    scales = (w & 0xFFFF).to(torch.int16).view(torch.float16)
+    zeros = (w >> 16).to(torch.int16)
+    return scales, zeros
+
+
+def join_sz(scales: torch.Tensor, zeros: torch.Tensor) -> torch.Tensor:
+    """(scales fp16 [N, G], integral zeros [N, G]) -> qsz [ceil(N/16), G, 16]."""
+    N, G = scales.shape
+    nt = -(-N // TILE_N)
+    lo = scales.contiguous().view(torch.int16).to(torch.int32) & 0xFFFF
+    hi = zeros.to(torch.int32) << 16
+    w = torch.zeros(nt * TILE_N, G, dtype=torch.int32, device=scales.device)
+    w[:N] = lo | hi
+    return w.view(nt, TILE_N, G).permute(0, 2, 1).contiguous()
+
+
+def sz_flags(qsz: torch.Tensor) -> int:
+    """QLIN_WIDE_ZERO if some zero point is outside +-1024 (degenerate groups only)."""
+    if qsz.numel() == 0:
+        return 0
+    return WIDE_ZERO if int((qsz >> 16).abs().max()) > WIDE_LIMIT else 0
+
+
 def quantize(x: torch.Tensor, bits: int, group: int, flags: int = 0, up_sig=None, low_sig=None,
              want_xdq=True, want_params=True, pack=False):
     """Fused calibrate + fake-quant (+ pack) of ``x`` viewed as [rows, K]; ``group`` divides K.
 
     Returns dict with ``x_dq`` [rows, K], ``scale`` / ``zp`` [rows*K/group] and, if ``pack``,
-    ``qweight`` / ``scales`` / ``zeros`` (int16)."""
+    ``qweight`` / ``qsz`` (tiled layout) and ``flags`` (layout flags for dequant / linear)."""
     _dev(x, up_sig, low_sig)
     K = x.shape[-1]
     rows = x.numel() // K if K else 0
@@ -121,18 +172,18 @@ def quantize(x: torch.Tensor, bits: int, group: int, flags: int = 0, up_sig=None
     scale = torch.empty(ng, dtype=x.dtype, device=x.device) if want_params else None
     zp = torch.empty(ng, dtype=x.dtype, device=x.device) if (
         want_params and not flags & DISABLE_ZERO_POINT) else None
-    qw = sc = z16 = None
+    qw = qsz = None
     if pack:
-        qw = torch.empty(rows, K * bits // 32, dtype=torch.int32, device=x.device)
-        sc = torch.empty(rows, K // group, dtype=torch.float16, device=x.device)
-        z16 = torch.empty(rows, K // group, dtype=torch.int16, device=x.device)
+        if group <= 0 or K % group:
+            raise ValueError(f"group {group} must divide K {K}")
+        qw, qsz = _alloc_packed(rows, K, bits, group, x.device)
     rc = load_library().qlin_quantize(
         _ptr(x), _dtcode(x), rows, K, bits, group, flags, _ptr(up_sig), _ptr(low_sig),
-        _ptr(xdq), _ptr(scale), _ptr(zp), _ptr(qw), _ptr(sc), _ptr(z16), _stream(x))
+        _ptr(xdq), _ptr(scale), _ptr(zp), _ptr(qw), _ptr(qsz), _stream(x))
     _check(rc, "qlin_quantize")
     out.update(x_dq=xdq, scale=scale, zp=zp)
     if pack:
-        out.update(qweight=qw, scales=sc, zeros=z16)
+        out.update(qweight=qw, qsz=qsz, flags=sz_flags(qsz))
     return out
 
 
@@ -143,76 +194,70 @@ def fake_quant(x: torch.Tensor, scale: torch.Tensor, zp, bits: int, group: int, 
     K = x.shape[-1]
     rows = x.numel() // K
     xdq = torch.empty_like(x) if want_xdq else None
-    qw = sc = z16 = None
+    qw = qsz = None
     if pack:
-        qw = torch.empty(rows, K * bits // 32, dtype=torch.int32, device=x.device)
-        sc = torch.empty(rows, K // group, dtype=torch.float16, device=x.device)
-        z16 = torch.empty(rows, K // group, dtype=torch.int16, device=x.device)
+        if group <= 0 or K % group:
+            raise ValueError(f"group {group} must divide K {K}")
+        qw, qsz = _alloc_packed(rows, K, bits, group, x.device)
     if scale.dtype != x.dtype or (zp is not None and zp.dtype != x.dtype):
         raise ValueError("scale / zero point dtype must match x")
     rc = load_library().qlin_fake_quant(
         _ptr(x), _dtcode(x), _ptr(scale), _ptr(zp), rows, K, bits, group, flags, _ptr(xdq),
-        _ptr(qw), _ptr(sc), _ptr(z16), _stream(x))
+        _ptr(qw), _ptr(qsz), _stream(x))
     _check(rc, "qlin_fake_quant")
-    return dict(x_dq=xdq, qweight=qw, scales=sc, zeros=z16)
+    return dict(x_dq=xdq, qweight=qw, qsz=qsz, flags=sz_flags(qsz) if pack else 0)
 
 
-def narrow_zeros(z16: torch.Tensor) -> torch.Tensor:
-    """int16 zero points -> int8 when every value fits (the common case), else keep int16."""
-    if z16.numel() == 0:
-        return z16.to(torch.int8)
-    lo, hi = torch.aminmax(z16)
-    if int(lo) >= -128 and int(hi) <= 127:
-        return z16.to(torch.int8)
-    return z16
+def _check_packed(qweight, qsz, N, K, bits, group):
+    if group <= 0 or K % group:
+        raise ValueError(f"group {group} must divide K {K}")
+    if tuple(qweight.shape) != packed_shape(N, K, bits) or qweight.dtype != torch.int32:
+        raise ValueError(f"qweight must be int32 {packed_shape(N, K, bits)}, got "
+                         f"{qweight.dtype} {tuple(qweight.shape)}")
+    if tuple(qsz.shape) != sz_shape(N, K, group) or qsz.dtype != torch.int32:
+        raise ValueError(f"qsz must be int32 {sz_shape(N, K, group)}, got "
+                         f"{qsz.dtype} {tuple(qsz.shape)}")
 
 
-def zero_bits(zeros: torch.Tensor) -> int:
-    if zeros.dtype == torch.int8:
-        return 8
-    if zeros.dtype == torch.int16:
-        return 16
-    raise ValueError(f"zeros must be int8 / int16, got {zeros.dtype}")
-
-
-def dequant(qweight, scales, zeros, N: int, K: int, bits: int, group: int) -> torch.Tensor:
-    _dev(qweight, scales, zeros)
+def dequant(qweight, qsz, N: int, K: int, bits: int, group: int, flags: int = 0) -> torch.Tensor:
+    _dev(qweight, qsz)
+    _check_packed(qweight, qsz, N, K, bits, group)
     w = torch.empty(N, K, dtype=torch.float16, device=qweight.device)
-    rc = load_library().qlin_dequant_f16(_ptr(qweight), _ptr(scales), _ptr(zeros),
-                                         zero_bits(zeros), N, K, bits, group, _ptr(w),
-                                         _stream(qweight))
+    rc = load_library().qlin_dequant_f16(_ptr(qweight), _ptr(qsz), flags, N, K, bits, group,
+                                         _ptr(w), _stream(qweight))
     _check(rc, "qlin_dequant_f16")
     return w
 
 
-def _linear_call(fn_name, x, qweight, scales, zeros, bias, N, K, bits, group, extra=()):
-    _dev(x, qweight, scales, zeros, bias)
+def _linear_call(fn_name, x, qweight, qsz, bias, N, K, bits, group, flags, extra=()):
+    _dev(x, qweight, qsz, bias)
     if x.dtype != torch.float16:
         raise ValueError(f"packed linear takes fp16 activations, got {x.dtype}")
     if x.shape[-1] != K:
         raise ValueError(f"input has {x.shape[-1]} features, layer expects {K}")
     if bias is not None and (bias.dtype != torch.float16 or bias.numel() != N):
         raise ValueError("bias must be fp16 [N]")
+    _check_packed(qweight, qsz, N, K, bits, group)
     M = x.numel() // K if K else 0
     y = torch.empty(*x.shape[:-1], N, dtype=torch.float16, device=x.device)
     if M == 0:
         return y
     fn = getattr(load_library(), fn_name)
-    rc = fn(_ptr(qweight), _ptr(scales), _ptr(zeros), zero_bits(zeros), _ptr(x), _ptr(bias),
-            _ptr(y), M, N, K, bits, group, *extra, _stream(x))
+    rc = fn(_ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(bias), _ptr(y), M, N, K, bits, group,
+            *extra, _stream(x))
     _check(rc, fn_name)
     return y
 
 
-def linear(x, qweight, scales, zeros, bias, N, K, bits, group):
+def linear(x, qweight, qsz, bias, N, K, bits, group, flags=0):
     """Dispatching fused dequant-matmul (GEMV for M <= 4, MFMA GEMM otherwise)."""
-    return _linear_call("qlin_linear_f16", x, qweight, scales, zeros, bias, N, K, bits, group)
+    return _linear_call("qlin_linear_f16", x, qweight, qsz, bias, N, K, bits, group, flags)
 
 
-def gemv(x, qweight, scales, zeros, bias, N, K, bits, group):
-    return _linear_call("qlin_gemv_f16", x, qweight, scales, zeros, bias, N, K, bits, group)
+def gemv(x, qweight, qsz, bias, N, K, bits, group, flags=0):
+    return _linear_call("qlin_gemv_f16", x, qweight, qsz, bias, N, K, bits, group, flags)
 
 
-def gemm(x, qweight, scales, zeros, bias, N, K, bits, group):
-    return _linear_call("qlin_gemm_f16", x, qweight, scales, zeros, bias, N, K, bits, group,
+def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0):
+    return _linear_call("qlin_gemm_f16", x, qweight, qsz, bias, N, K, bits, group, flags,
                         extra=(None,))

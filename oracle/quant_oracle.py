@@ -16,15 +16,14 @@ binary fp16 op as "compute in float32, round once to fp16" (verified: 0 mismatch
 divisions / multiplications).  ``_op`` restates exactly that: inputs are upcast to float32, the
 op is evaluated in IEEE float32 and the result is rounded (nearest-even) to the compute dtype.
 
-Canonical packed layout (the build's own format):
-  qweight  uint32 [N, K*bits/32]; each row is a sequence of 32-element "lane chunks", each chunk
-           ``bits`` words.  For bits in {2,4,8} word i of a chunk holds elements
-           k = i*2P + 2p + h (P = 16/bits pairs per word, p < P, h in {0,1}) at bit 16*h + bits*p,
-           so ``(w >> bits*p) & mask16x2`` yields the fp16-mantissa pair (k, k+1).
-           bits == 3: words 0,1 hold the low two bits of the 32 values in the bits==2 layout and
-           word 2 holds bit 2 of element 2p+h at bit 16*h + p.
-  scales   fp16  [N, K/g]  (== reference ``scales.view(N, -1)``, omniquant.py:322-325)
-  zeros    int8 or int16 [N, K/g]  (integral zero point; int16 when any |zp| > 127)
+Canonical packed layout (the build's own format, see DESIGN.md §3 and ``pack_qweight``):
+  qweight  uint32 [ceil(N/16), ceil(K/128), 64, bits]: 16-row x 128-k tiles of 64 lane pieces,
+           lane l = n + 16q holding codes (s, j) of row n at k = 32s + 8q + j (s, j < 4, 8) — the
+           B operand of v_mfma_f32_16x16x32_f16 k-step s; inside a piece the codes sit so that one
+           v_and_or_b32 with an fp16 exponent "magic" yields the pair (off + u_j, off + u_j+1).
+  qsz      uint32 [ceil(N/16), K/g, 16]: per (16-row tile, group, row) the fp16 scale (bits 0-15,
+           == reference ``scales.view(N, -1)``, omniquant.py:322-325) and the int16 zero point
+           (bits 16-31, == ``zeros.view(N, -1)``); one coalesced 64-B load per tile and group.
 """
 from __future__ import annotations
 
@@ -157,70 +156,117 @@ def quantize(w, n_bits, group_size=None, symmetric=False, disable_zero_point=Fal
 
 
 # ----------------------------------------------------------------------------------------------
-# canonical packed layout (build-defined; consumed by the HIP kernels)
+# canonical packed layout (build-defined; consumed by the HIP kernels) — "qlin tiled" layout
 # ----------------------------------------------------------------------------------------------
+TILE_N = 16    # rows per tile (the 16 columns of a v_mfma_f32_16x16x32_f16 B operand)
+TILE_K = 128   # k per tile (4 MFMA k-steps of 32)
+RHO3 = (0, 1, 8, 9)  # int3 high-bit word rotation per k-step
 
-def _pairs_per_word(bits):
-    return 16 // bits
+
+def tiled_shape(N, K, bits):
+    return (-(-N // TILE_N), -(-K // TILE_K), 64, bits)
+
+
+def _code_bit(bits, s, j):
+    """(word, bit) of code (step s, j) inside a lane piece for bits in {2,4,8}."""
+    p, h = j >> 1, j & 1
+    if bits == 4:
+        return s, 16 * h + 4 * p
+    if bits == 8:
+        jj = j & 3
+        return 2 * s + (j >> 2), 16 * h + 8 * (jj >> 1)
+    if bits == 2:
+        return s >> 1, 16 * h + 8 * (s & 1) + 2 * p
+    raise ValueError(bits)
 
 
 def pack_qweight(u, bits):
-    """Pack unsigned integer codes ``u`` [N, K] (0 <= u < 2**bits) into the canonical layout."""
+    """Pack unsigned codes ``u`` [N, K] (0 <= u < 2**bits, K % 32 == 0) into the tiled layout.
+
+    Tile (nt, kt) = rows 16nt..16nt+15 x k 128kt..128kt+127, stored as 64 lane pieces of ``bits``
+    uint32.  Lane l = n + 16q (n = l & 15, q = l >> 4) holds the 32 codes (s, j), s = 0..3,
+    j = 0..7, of row 16nt + n at k = 128kt + 32s + 8q + j — exactly the B operand lane l feeds to
+    MFMA k-step s.  Rows / k beyond (N, K) are zero codes."""
     u = np.asarray(u, dtype=np.uint32)
     N, K = u.shape
     assert K % 32 == 0, "K must be a multiple of 32"
-    ch = u.reshape(N, K // 32, 32)
+    Nt, Kt = -(-N // TILE_N), -(-K // TILE_K)
+    up = np.zeros((Nt * TILE_N, Kt * TILE_K), dtype=np.uint32)
+    up[:N, :K] = u
+    # c[nt, kt, n, s, q, j]
+    c = up.reshape(Nt, TILE_N, Kt, 4, 4, 8).transpose(0, 2, 1, 3, 4, 5)
+    out = np.zeros((Nt, Kt, 4, TILE_N, bits), dtype=np.uint32)  # [nt, kt, q, n, word]
     if bits in (2, 4, 8):
-        P = _pairs_per_word(bits)
-        words = np.zeros((N, K // 32, bits), dtype=np.uint32)
-        for i in range(bits):
-            for p in range(P):
-                for h in range(2):
-                    k = i * 2 * P + 2 * p + h
-                    words[:, :, i] |= ch[:, :, k] << np.uint32(16 * h + bits * p)
+        for s in range(4):
+            for j in range(8):
+                w, b = _code_bit(bits, s, j)
+                out[:, :, :, :, w] |= (c[:, :, :, s, :, j].transpose(0, 1, 3, 2) << np.uint32(b))
     elif bits == 3:
-        lo = pack_qweight(u & 3, 2).reshape(N, K // 32, 2)
-        hi = np.zeros((N, K // 32, 1), dtype=np.uint32)
-        for p in range(16):
-            for h in range(2):
-                hi[:, :, 0] |= ((ch[:, :, 2 * p + h] >> np.uint32(2)) & np.uint32(1)) << np.uint32(16 * h + p)
-        words = np.concatenate([lo, hi], axis=2)
+        lo = c & np.uint32(3)
+        for s in range(4):
+            for j in range(8):
+                w, b = _code_bit(2, s, j)
+                out[:, :, :, :, w] |= (lo[:, :, :, s, :, j].transpose(0, 1, 3, 2) << np.uint32(b))
+                p, h = j >> 1, j & 1
+                hb = (16 * h + 2 * p + 2 + RHO3[s]) % 32
+                hi = (c[:, :, :, s, :, j] >> np.uint32(2)) & np.uint32(1)
+                out[:, :, :, :, 2] |= (hi.transpose(0, 1, 3, 2) << np.uint32(hb))
     else:
         raise ValueError(f"bits={bits} not supported")
-    return words.reshape(N, K * bits // 32)
+    return out.reshape(Nt, Kt, 64, bits)
 
 
-def unpack_qweight(qw, bits, K):
-    """Inverse of ``pack_qweight``."""
+def unpack_qweight(qw, bits, N, K):
+    """Inverse of ``pack_qweight``: codes [N, K]."""
     qw = np.asarray(qw, dtype=np.uint32)
-    N = qw.shape[0]
-    words = qw.reshape(N, K // 32, bits)
-    out = np.zeros((N, K // 32, 32), dtype=np.uint32)
-    if bits in (2, 4, 8):
-        P = _pairs_per_word(bits)
-        m = np.uint32(2 ** bits - 1)
-        for i in range(bits):
-            for p in range(P):
-                for h in range(2):
-                    out[:, :, i * 2 * P + 2 * p + h] = (words[:, :, i] >> np.uint32(16 * h + bits * p)) & m
-    elif bits == 3:
-        lo = unpack_qweight(words[:, :, :2].reshape(N, -1), 2, K).reshape(N, K // 32, 32)
-        out[:] = lo
-        for p in range(16):
-            for h in range(2):
-                out[:, :, 2 * p + h] |= ((words[:, :, 2] >> np.uint32(16 * h + p)) & np.uint32(1)) << np.uint32(2)
-    else:
-        raise ValueError(f"bits={bits} not supported")
-    return out.reshape(N, K)
+    Nt, Kt = qw.shape[0], qw.shape[1]
+    words = qw.reshape(Nt, Kt, 4, TILE_N, bits)  # [nt, kt, q, n, word]
+    c = np.zeros((Nt, Kt, TILE_N, 4, 4, 8), dtype=np.uint32)  # [nt, kt, n, s, q, j]
+    for s in range(4):
+        for j in range(8):
+            if bits in (2, 4, 8):
+                w, b = _code_bit(bits, s, j)
+                v = (words[..., w] >> np.uint32(b)) & np.uint32(2 ** bits - 1)
+            else:
+                w, b = _code_bit(2, s, j)
+                p, h = j >> 1, j & 1
+                hb = (16 * h + 2 * p + 2 + RHO3[s]) % 32
+                v = ((words[..., w] >> np.uint32(b)) & np.uint32(3)) | \
+                    (((words[..., 2] >> np.uint32(hb)) & np.uint32(1)) << np.uint32(2))
+            c[:, :, :, s, :, j] = v.transpose(0, 1, 3, 2)
+    full = c.transpose(0, 2, 1, 3, 4, 5).reshape(Nt * TILE_N, Kt * TILE_K)
+    return full[:N, :K]
 
 
-def zero_dtype_for(z):
-    z = np.asarray(z)
-    return np.int8 if (z.size == 0 or (z.min() >= -128 and z.max() <= 127)) else np.int16
+WIDE_ZERO = 1024  # |zp| above this needs the kernels' fp32 (u - zp) path (QLIN_WIDE_ZERO)
+
+
+def pack_sz(scales, zeros):
+    """Packed (scale, zero) words: uint32 [ceil(N/16), G, 16]; word (nt, g, n) holds the fp16 bits
+    of scales[16nt + n, g] in bits 0..15 and the int16 zero point in bits 16..31 (rows >= N: 0)."""
+    sc = np.asarray(scales, dtype=F16).reshape(np.asarray(scales).shape[0], -1)
+    N, G = sc.shape
+    z = np.asarray(zeros).reshape(N, G).astype(np.int64)
+    assert z.min(initial=0) >= -32768 and z.max(initial=0) <= 32767
+    Nt = -(-N // TILE_N)
+    w = np.zeros((Nt * TILE_N, G), dtype=np.uint32)
+    w[:N] = sc.view(np.uint16).astype(np.uint32) | ((z.astype(np.int16).view(np.uint16).astype(np.uint32)) << np.uint32(16))
+    return w.reshape(Nt, TILE_N, G).transpose(0, 2, 1).copy()
+
+
+def unpack_sz(qsz, N):
+    """Inverse of ``pack_sz``: (scales fp16 [N, G], zeros int32 [N, G])."""
+    qsz = np.asarray(qsz, dtype=np.uint32)
+    Nt, G, _ = qsz.shape
+    w = qsz.transpose(0, 2, 1).reshape(Nt * TILE_N, G)[:N]
+    sc = (w & np.uint32(0xFFFF)).astype(np.uint16).view(F16)
+    z = (w >> np.uint32(16)).astype(np.uint16).view(np.int16).astype(np.int32)
+    return sc, z
 
 
 def pack_from_quant(x_int, scale, rzp, n_bits, N, K, group_size, disable_zero_point=False):
-    """Canonical packed tensors from the quantizer's integer codes and fp16 (scale, zp)."""
+    """Canonical packed tensors (qweight, qsz, wide) from the quantizer's integer codes and fp16
+    (scale, zp)."""
     g = group_size or K
     if disable_zero_point:
         off = 2 ** (n_bits - 1)
@@ -231,14 +277,14 @@ def pack_from_quant(x_int, scale, rzp, n_bits, N, K, group_size, disable_zero_po
         zeros = np.asarray(rzp, dtype=np.float32).reshape(N, K // g).astype(np.int32)
     qweight = pack_qweight(u.astype(np.uint32), n_bits)
     scales = np.asarray(scale, dtype=F16).reshape(N, K // g)
-    zeros = zeros.astype(zero_dtype_for(zeros))
-    return qweight, scales, zeros
+    wide = bool(zeros.size and np.abs(zeros).max() > WIDE_ZERO)
+    return qweight, pack_sz(scales, zeros), wide
 
 
 def pack_from_dequant(w_dq, scales, zeros, n_bits, group_size, disable_zero_point=False):
     """Restatement of the real-quant packer input contract (omniquant.py:315-335): recover integer
     codes from ``W_dq`` and the registered fp16 (scales, zeros) with the quantizer's own fp16
-    arithmetic, then pack.  Returns ``(qweight, scales, zeros)`` in the canonical layout."""
+    arithmetic, then pack.  Returns ``(qweight, qsz, wide)`` in the canonical layout."""
     N, K = w_dq.shape
     g = group_size or K
     qmin, qmax = qrange(n_bits, disable_zero_point)
@@ -253,14 +299,14 @@ def pack_from_dequant(w_dq, scales, zeros, n_bits, group_size, disable_zero_poin
                            group_size, disable_zero_point)
 
 
-def dequant_packed(qweight, scales, zeros, n_bits, K, group_size=None):
+def dequant_packed(qweight, qsz, n_bits, N, K, group_size=None):
     """W_dq = RN16( RN16(q - zp) * s ) from the canonical layout (fp16, bit-exact with the
     reference's ``x_dequant.sub(zp).mul(scale)``, quantizer.py:107-110)."""
-    N = qweight.shape[0]
     g = group_size or K
-    u = unpack_qweight(qweight, n_bits, K).astype(np.float32).reshape(N, K // g, g)
-    z = np.asarray(zeros, dtype=np.float32).reshape(N, K // g, 1)
-    s = np.asarray(scales, dtype=F16).reshape(N, K // g, 1)
+    sc, zr = unpack_sz(qsz, N)
+    u = unpack_qweight(qweight, n_bits, N, K).astype(np.float32).reshape(N, K // g, g)
+    z = zr.astype(np.float32).reshape(N, K // g, 1)
+    s = sc.reshape(N, K // g, 1)
     v = (u - z).astype(F16)  # exact integer, one fp16 rounding (matches RN16(x_int - zp))
     return _op(np.multiply, F16, v, s).reshape(N, K)
 

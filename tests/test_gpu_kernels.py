@@ -78,21 +78,26 @@ def test_pack_and_dequant_bit_exact(name):
     _, scale, zp, x_int = O.quantize(g["w"], p["n_bits"], p["group_size"], p["symmetric"],
                                      p["disable_zero_point"])
     ok = ~np.isnan(g["w_dq"]).any(axis=1)
-    oq, osc, oz = O.pack_from_quant(np.nan_to_num(x_int), scale, zp, p["n_bits"], N, K,
-                                    p["group_size"], p["disable_zero_point"])
-    assert np.array_equal(n(out["qweight"]).view(np.uint32)[ok], oq[ok])
-    assert bit_equal(n(out["scales"]), osc)
-    assert np.array_equal(n(out["zeros"]).astype(np.int32), oz.astype(np.int32))
-    z = qlin.narrow_zeros(out["zeros"])
-    w = qlin.dequant(out["qweight"], out["scales"], z, N, K, p["n_bits"], grp)
+    oq, osz, owide = O.pack_from_quant(np.nan_to_num(x_int), scale, zp, p["n_bits"], N, K,
+                                       p["group_size"], p["disable_zero_point"])
+    gq = n(out["qweight"]).view(np.uint32)
+    assert gq.shape == oq.shape
+    if ok.all():
+        assert np.array_equal(gq, oq)  # the kernel's packed words are the oracle's, bit for bit
+    assert np.array_equal(O.unpack_qweight(gq, p["n_bits"], N, K)[ok],
+                          O.unpack_qweight(oq, p["n_bits"], N, K)[ok])
+    gsz = n(out["qsz"]).view(np.uint32)
+    assert gsz.shape == osz.shape
+    assert np.array_equal(gsz, osz)  # (scale, zero) words bit for bit
+    assert (out["flags"] == qlin.WIDE_ZERO) == owide
+    w = qlin.dequant(out["qweight"], out["qsz"], N, K, p["n_bits"], grp, out["flags"])
     assert bit_equal(n(w)[ok], g["w_dq"][ok])
     # the real-quant packer: codes recovered from (W_dq, scales, zeros) alone
     wdq = np.where(ok[:, None], g["w_dq"], 0).astype(np.float16)
     pz = None if p["disable_zero_point"] else t(g["zp"].reshape(-1))
     out2 = qlin.fake_quant(t(wdq), t(g["scale"].reshape(-1)), pz, p["n_bits"], grp,
                            flags & qlin.DISABLE_ZERO_POINT, want_xdq=False, pack=True)
-    w2 = qlin.dequant(out2["qweight"], out2["scales"], qlin.narrow_zeros(out2["zeros"]), N, K,
-                      p["n_bits"], grp)
+    w2 = qlin.dequant(out2["qweight"], out2["qsz"], N, K, p["n_bits"], grp, out2["flags"])
     assert bit_equal(n(w2)[ok], g["w_dq"][ok])
 
 
@@ -102,13 +107,12 @@ def _packed(N, K, bits, group, seed, wide=False):
         W[: max(1, N // 7), :group] = 1.0 + np.random.RandomState(seed).rand(
             max(1, N // 7), group).astype(np.float16) * np.float16(1e-3)
     out = qlin.quantize(t(W), bits, group, 0, pack=True)
-    z = qlin.narrow_zeros(out["zeros"])
-    wdq = n(qlin.dequant(out["qweight"], out["scales"], z, N, K, bits, group))
-    return out["qweight"], out["scales"], z, wdq
+    wdq = n(qlin.dequant(out["qweight"], out["qsz"], N, K, bits, group, out["flags"]))
+    return out["qweight"], out["qsz"], out["flags"], wdq
 
 
 GEMV_SHAPES = [(4096, 4096, 128), (1024, 4096, 128), (777, 768, 128), (300, 3072, 64),
-               (130, 14336, 128), (64, 32, 32), (96, 512, 512)]
+               (130, 14336, 128), (64, 32, 32), (96, 512, 512), (50, 96, 32), (40, 4096, 4096)]
 
 
 @pytest.mark.parametrize("bits", [4, 3, 2, 8])
@@ -117,12 +121,12 @@ def test_gemv_matches_oracle(bits, shape):
     N, K, group = shape
     if bits in (2, 3) and group == 128:
         group = 64 if K % 64 == 0 else group
-    qw, sc, z, wdq = _packed(N, K, bits, group, seed=N + K + bits)
+    qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=N + K + bits)
     bias = np.random.RandomState(3).randn(N).astype(np.float16) * np.float16(0.1)
     for M in (1, 2, 3, 4):
         x = rand_x(M, K, seed=M)
         for b in (None, bias):
-            y = qlin.gemv(t(x), qw, sc, z, None if b is None else t(b), N, K, bits, group)
+            y = qlin.gemv(t(x), qw, qsz, None if b is None else t(b), N, K, bits, group, fl)
             ref = O.linear_ref(x, wdq, b)
             assert_close_to_ref(n(y), ref, what=f"gemv b{bits} M{M} N{N} K{K} g{group}")
 
@@ -130,15 +134,20 @@ def test_gemv_matches_oracle(bits, shape):
 @pytest.mark.parametrize("wide", [False, True])
 def test_gemv_wide_zeros(wide):
     N, K, group = 512, 1024, 128
-    qw, sc, z, wdq = _packed(N, K, 4, group, seed=5, wide=wide)
-    assert (z.dtype == torch.int16) == wide
-    x = rand_x(1, K, 9)
-    y = qlin.gemv(t(x), qw, sc, z, None, N, K, 4, group)
-    assert_close_to_ref(n(y), O.linear_ref(x, wdq), what="wide")
+    qw, qsz, fl, wdq = _packed(N, K, 4, group, seed=5, wide=wide)
+    assert (fl == qlin.WIDE_ZERO) == wide
+    for M in (1, 3):
+        x = rand_x(M, K, 9)
+        y = qlin.gemv(t(x), qw, qsz, None, N, K, 4, group, fl)
+        assert_close_to_ref(n(y), O.linear_ref(x, wdq), what="wide gemv")
+    x = rand_x(40, K, 9)
+    y = qlin.gemm(t(x), qw, qsz, None, N, K, 4, group, fl)
+    assert_close_to_ref(n(y), O.linear_ref(x, wdq), what="wide gemm")
 
 
 GEMM_SHAPES = [(5, 4096, 4096, 128), (33, 1024, 4096, 128), (128, 777, 768, 128),
-               (300, 256, 3072, 64), (200, 4096, 14336, 128), (2048, 512, 1024, 128)]
+               (300, 256, 3072, 64), (200, 4096, 14336, 128), (2048, 512, 1024, 128),
+               (17, 100, 96, 32), (129, 136, 160, 32)]
 
 
 @pytest.mark.parametrize("bits", [4, 3, 2, 8])
@@ -147,32 +156,39 @@ def test_gemm_matches_oracle(bits, shape):
     M, N, K, group = shape
     if bits in (2, 3) and group == 128:
         group = 64
-    qw, sc, z, wdq = _packed(N, K, bits, group, seed=M + N + K + bits)
+    qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=M + N + K + bits)
     x = rand_x(M, K, seed=M)
     bias = np.random.RandomState(4).randn(N).astype(np.float16) * np.float16(0.1)
-    y = qlin.gemm(t(x), qw, sc, z, t(bias), N, K, bits, group)
+    y = qlin.gemm(t(x), qw, qsz, t(bias), N, K, bits, group, fl)
     assert_close_to_ref(n(y), O.linear_ref(x, wdq, bias), what=f"gemm b{bits} {shape}")
 
 
 def test_linear_dispatch_and_batch_shapes():
     N, K, group = 384, 1024, 128
-    qw, sc, z, wdq = _packed(N, K, 4, group, seed=11)
+    qw, qsz, fl, wdq = _packed(N, K, 4, group, seed=11)
     for shp in ((1, 1, K), (1, 3, K), (2, 5, K), (1, 64, K)):
         x = np.random.RandomState(len(shp)).randn(*shp).astype(np.float16)
-        y = qlin.linear(t(x), qw, sc, z, None, N, K, 4, group)
+        y = qlin.linear(t(x), qw, qsz, None, N, K, 4, group, fl)
         assert tuple(y.shape) == shp[:-1] + (N,)
         assert_close_to_ref(n(y).reshape(-1, N), O.linear_ref(x.reshape(-1, K), wdq))
 
 
 def test_invalid_arguments_raise():
     N, K, group = 64, 256, 128
-    qw, sc, z, _ = _packed(N, K, 4, group, seed=1)
+    qw, qsz, fl, _ = _packed(N, K, 4, group, seed=1)
     x = t(rand_x(1, K, 1))
     with pytest.raises(ValueError):
-        qlin.gemv(x, qw, sc, z, None, N, K, 5, group)          # bits
+        qlin.gemv(x, qw, qsz, None, N, K, 5, group)            # bits
     with pytest.raises(ValueError):
-        qlin.gemv(x, qw, sc, z, None, N, K, 4, 100)            # group
+        qlin.gemv(x, qw, qsz, None, N, K, 4, 100)              # group
     with pytest.raises(ValueError):
-        qlin.linear(x.float(), qw, sc, z, None, N, K, 4, group)  # dtype
+        qlin.linear(x.float(), qw, qsz, None, N, K, 4, group)  # dtype
     with pytest.raises(RuntimeError):
-        qlin.linear(x.cpu(), qw, sc, z, None, N, K, 4, group)    # CPU tensor: no fallback
+        qlin.linear(x.cpu(), qw, qsz, None, N, K, 4, group)    # CPU tensor: no fallback
+    lib = qlin.load_library()
+    y = torch.empty(1, N, dtype=torch.float16, device="cuda")
+    # raw C ABI: M out of the GEMV range, null pointers
+    assert lib.qlin_gemv_f16(qw.data_ptr(), qsz.data_ptr(), 0, x.data_ptr(), None, y.data_ptr(),
+                             5, N, K, 4, group, None) == 1
+    assert lib.qlin_gemm_f16(None, qsz.data_ptr(), 0, x.data_ptr(), None, y.data_ptr(),
+                             1, N, K, 4, group, None, None) == 1

@@ -39,16 +39,21 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     from quant import qlin
     lib = qlin.load_library()
     # every entry point validates before touching the device
-    assert lib.qlin_dequant_f16(None, None, None, 8, 16, 64, 4, 64, None, None) == 1
-    assert lib.qlin_gemv_f16(None, None, None, 8, None, None, None, 1, 16, 64, 4, 64, None) == 1
-    assert lib.qlin_gemm_f16(None, None, None, 8, None, None, None, 8, 16, 64, 4, 64, None, None) == 1
+    assert lib.qlin_dequant_f16(None, None, 0, 16, 64, 4, 64, None, None) == 1
+    assert lib.qlin_gemv_f16(None, None, 0, None, None, None, 1, 16, 64, 4, 64, None) == 1
+    assert lib.qlin_gemm_f16(None, None, 0, None, None, None, 8, 16, 64, 4, 64, None, None) == 1
     assert lib.qlin_quantize(None, 0, 4, 64, 4, 64, 0, None, None, None, None, None, None, None,
-                             None, None) == 1
+                             None) == 1
+    assert lib.qlin_fake_quant(None, 0, None, None, 4, 64, 4, 64, 0, None, None, None, None) == 1
+    assert lib.qlin_pack_f16(None, None, None, 4, 64, 4, 64, 0, None, None, None) == 1
     p = ctypes.c_void_p(16)  # never dereferenced: the shape check fails first
-    assert lib.qlin_gemv_f16(p, p, p, 8, p, None, p, 1, 16, 65, 4, 64, None) == 1   # K % 32
-    assert lib.qlin_gemv_f16(p, p, p, 8, p, None, p, 9, 16, 64, 4, 64, None) == 1   # M > 4
-    assert lib.qlin_gemv_f16(p, p, p, 8, p, None, p, 1, 16, 64, 5, 64, None) == 1   # bits
-    assert lib.qlin_gemv_f16(p, p, p, 12, p, None, p, 1, 16, 64, 4, 64, None) == 1  # zero bits
+    assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 1, 16, 65, 4, 64, None) == 1   # K % 32
+    assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 9, 16, 64, 4, 64, None) == 1   # M > 4
+    assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 1, 16, 64, 5, 64, None) == 1   # bits
+    assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 1, 16, 128, 4, 96, None) == 1  # group | K
+    assert lib.qlin_gemm_f16(p, p, 0, p, None, p, 8, 16, 64, 4, 48, None, None) == 1  # group % 32
+    assert lib.qlin_linear_f16(p, p, 0, p, None, p, 8, -1, 64, 4, 64, None) == 1  # N < 0
+    assert lib.qlin_dequant_f16(p, p, 0, 16, 64, 3, 128, p, None) == 1  # group > K
     assert lib.qlin_error_string(1) == b"invalid argument"
 
 

@@ -65,28 +65,65 @@ def test_act_per_token_bit_exact(name):
 
 
 @pytest.mark.parametrize("bits", [2, 3, 4, 8])
-def test_pack_roundtrip(bits):
+@pytest.mark.parametrize("shape", [(7, 256), (16, 128), (33, 96), (48, 4096)])
+def test_pack_roundtrip(bits, shape):
     rs = np.random.RandomState(bits)
-    u = rs.randint(0, 2 ** bits, size=(7, 256)).astype(np.uint32)
+    u = rs.randint(0, 2 ** bits, size=shape).astype(np.uint32)
     qw = O.pack_qweight(u, bits)
-    assert qw.shape == (7, 256 * bits // 32) and qw.dtype == np.uint32
-    np.testing.assert_array_equal(O.unpack_qweight(qw, bits, 256), u)
+    assert qw.shape == O.tiled_shape(*shape, bits) and qw.dtype == np.uint32
+    np.testing.assert_array_equal(O.unpack_qweight(qw, bits, *shape), u)
 
 
-def test_pack_layout_int4_known_answer():
-    # element k of a chunk: word k//8, pair p=(k%8)//2, half h=k%2 -> bit 16h + 4p
-    u = np.arange(32, dtype=np.uint32)[None, :] % 16
-    qw = O.pack_qweight(u, 4)
-    w0 = 0
-    for k in range(8):
-        w0 |= (k % 16) << (16 * (k % 2) + 4 * (k // 2))
-    assert int(qw[0, 0]) == w0
-    # the fp16 magic unpack: ((w >> 4p) & 0x000F000F) | 0x64006400 -> (1024+u[2p], 1024+u[2p+1])
-    for p in range(4):
-        v = ((int(qw[0, 0]) >> (4 * p)) & 0x000F000F) | 0x64006400
-        lo = np.array([v & 0xFFFF], dtype=np.uint16).view(np.float16)[0]
-        hi = np.array([v >> 16], dtype=np.uint16).view(np.float16)[0]
-        assert (lo, hi) == (1024 + 2 * p, 1024 + 2 * p + 1)
+def _f16(v):
+    return float(np.array([v & 0xFFFF], dtype=np.uint16).view(np.float16)[0])
+
+
+MAGIC = {1024: 0x64006400, 256: 0x5C005C00, 64: 0x54005400, 16: 0x4C004C00}
+
+
+def kernel_extract(words, bits, s):
+    """The GEMV kernel's unpack of k-step s of one lane piece (qlin_common.h), simulated bit for bit:
+    returns the 8 fp16 values (off_j + u_j) and the offsets off_j."""
+    w = [int(x) for x in words]
+    pairs = []
+    if bits == 4:
+        ws = w[s]
+        for sh, mask, off in ((0, 0x000F000F, 1024), (0, 0x00F000F0, 64), (8, 0x000F000F, 1024),
+                              (8, 0x00F000F0, 64)):
+            pairs.append((((ws >> sh) & mask) | MAGIC[off], off))
+    elif bits == 8:
+        for ww in (w[2 * s], w[2 * s + 1]):
+            for sh in (0, 8):
+                pairs.append((((ww >> sh) & 0x00FF00FF) | MAGIC[1024], 1024))
+    else:
+        ws = w[s >> 1] >> (8 * (s & 1))
+        hs = ((w[2] >> O.RHO3[s]) | (w[2] << (32 - O.RHO3[s]))) & 0xFFFFFFFF if bits == 3 else 0
+        for p, off in enumerate((1024, 256, 64, 16)):
+            v = (ws & (0x00030003 << (2 * p))) | MAGIC[off]
+            if bits == 3:
+                v |= hs & (0x00040004 << (2 * p))
+            pairs.append((v, off))
+    vals, offs = [], []
+    for v, off in pairs:
+        vals += [_f16(v), _f16(v >> 16)]
+        offs += [off, off]
+    return vals, offs
+
+
+@pytest.mark.parametrize("bits", [2, 3, 4, 8])
+def test_magic_unpack_known_answer(bits):
+    """Every code of every lane piece decodes to exactly off + u with the kernel's bit operations,
+    and lane l = n + 16q, step s, element j is the code of row n at k = 32s + 8q + j."""
+    rs = np.random.RandomState(100 + bits)
+    N, K = 16, 128
+    u = rs.randint(0, 2 ** bits, size=(N, K)).astype(np.uint32)
+    qw = O.pack_qweight(u, bits)[0, 0]
+    for lane in range(64):
+        n, q = lane & 15, lane >> 4
+        for s in range(4):
+            vals, offs = kernel_extract(qw[lane], bits, s)
+            for j in range(8):
+                assert vals[j] - offs[j] == u[n, 32 * s + 8 * q + j], (lane, s, j)
 
 
 @pytest.mark.parametrize("name", ["q_w4g128_f16", "q_w3g64_f16", "q_w2g64_f16", "q_w8pc_f16",
@@ -102,24 +139,39 @@ def test_dequant_packed_matches_reference(name):
                                         p["disable_zero_point"], g.get("lwc_up"), g.get("lwc_low"))
     ok = ~np.isnan(w_dq).any(axis=1)
     x_int = np.nan_to_num(x_int)
-    qw, sc, z = O.pack_from_quant(x_int, scale, zp, p["n_bits"], N, K, p["group_size"],
-                                  p["disable_zero_point"])
-    assert z.dtype in (np.int8, np.int16)
-    dq = O.dequant_packed(qw, sc, z, p["n_bits"], K, p["group_size"])
+    qw, qsz, wide = O.pack_from_quant(x_int, scale, zp, p["n_bits"], N, K, p["group_size"],
+                                      p["disable_zero_point"])
+    sc, z = O.unpack_sz(qsz, N)
+    assert bit_equal(sc.reshape(-1, 1), scale.astype(np.float16))
+    dq = O.dequant_packed(qw, qsz, p["n_bits"], N, K, p["group_size"])
     assert bit_equal(dq[ok], g["w_dq"][ok])
     # real-quant packer contract: recover codes from (W_dq, scales, zeros) alone
-    qw2, sc2, z2 = O.pack_from_dequant(np.where(ok[:, None], g["w_dq"], 0).astype(np.float16),
+    qw2, qsz2, _ = O.pack_from_dequant(np.where(ok[:, None], g["w_dq"], 0).astype(np.float16),
                                        scale, zp, p["n_bits"], p["group_size"],
                                        p["disable_zero_point"])
-    dq2 = O.dequant_packed(qw2, sc2, z2, p["n_bits"], K, p["group_size"])
+    dq2 = O.dequant_packed(qw2, qsz2, p["n_bits"], N, K, p["group_size"])
     assert bit_equal(dq2[ok], g["w_dq"][ok])
 
 
-def test_wide_zero_uses_int16():
+def test_wide_zero_flag():
     g = load_golden("q_w3g64_f16")
     _, scale, zp, x_int = O.quantize(g["w"], 3, 64)
-    _, _, z = O.pack_from_quant(np.nan_to_num(x_int), scale, zp, 3, 64, 512, 64)
-    assert z.dtype == np.int16 and z.min() == -10000
+    _, qsz, wide = O.pack_from_quant(np.nan_to_num(x_int), scale, zp, 3, 64, 512, 64)
+    assert wide and O.unpack_sz(qsz, 64)[1].min() == -10000
+    g = load_golden("q_w4g128_f16")
+    _, scale, zp, x_int = O.quantize(g["w"], 4, 128)
+    assert not O.pack_from_quant(np.nan_to_num(x_int), scale, zp, 4, 64, 512, 128)[2]
+
+
+def test_sz_layout_roundtrip():
+    rs = np.random.RandomState(0)
+    sc = (rs.rand(37, 5) * 0.01).astype(np.float16)
+    z = rs.randint(-3000, 3000, size=(37, 5))
+    q = O.pack_sz(sc, z)
+    assert q.shape == (3, 5, 16)
+    s2, z2 = O.unpack_sz(q, 37)
+    assert bit_equal(s2, sc) and np.array_equal(z2, z)
+    assert int(q[1, 2, 3]) == (int(sc[19, 2].view(np.uint16)) | ((int(z[19, 2]) & 0xFFFF) << 16))
 
 
 @pytest.mark.parametrize("tag", ["f16", "f32"])
