@@ -144,8 +144,8 @@ def main():
         for i, (qw, qsz, fl) in enumerate(mats):
             y = ys[i % len(ys)]
             if kernel == "gemv":
-                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl, x.data_ptr(), None, y.data_ptr(),
-                        M, N, K, bits, group, st)
+                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl, x.data_ptr(), None,
+                        y.data_ptr(), M, N, K, bits, group, st)
             else:
                 rc = fn(qw.data_ptr(), qsz.data_ptr(), fl, x.data_ptr(), None, y.data_ptr(),
                         M, N, K, bits, group, None, st)
@@ -153,8 +153,10 @@ def main():
                 raise RuntimeError(f"kernel failed: {rc}")
 
     use_graph = not args.no_graph and kernel == "gemv"
-    graph = None
-    if use_graph:
+
+    def make_runner():
+        if not use_graph:
+            return step
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
@@ -163,9 +165,9 @@ def main():
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             step()
-        run = graph.replay
-    else:
-        run = step
+        return graph.replay
+
+    run = make_runner()
 
     for _ in range(args.warmup):
         run()

@@ -83,6 +83,31 @@ __device__ __forceinline__ Piece<BITS> load_piece(const uint32_t* __restrict__ p
   return c;
 }
 
+// the same with the non-temporal hint on the streamed (read-once) weight bytes: measured
+// -5 % per 4096 x 4096 GEMV launch (tools/dev/gemv_lab.hip); int3's 12-byte piece keeps the plain
+// load (no 3-dword vector type without 16-byte padding)
+template <int BITS>
+__device__ __forceinline__ Piece<BITS> load_piece_nt(const uint32_t* __restrict__ p) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  Piece<BITS> c;
+  if constexpr (BITS == 4) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    c.w[0] = v.x; c.w[1] = v.y; c.w[2] = v.z; c.w[3] = v.w;
+  } else if constexpr (BITS == 8) {
+    const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    const u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 4));
+    c.w[0] = a.x; c.w[1] = a.y; c.w[2] = a.z; c.w[3] = a.w;
+    c.w[4] = b.x; c.w[5] = b.y; c.w[6] = b.z; c.w[7] = b.w;
+  } else if constexpr (BITS == 2) {
+    const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+    c.w[0] = v.x; c.w[1] = v.y;
+  } else {
+    c = load_piece<BITS>(p);
+  }
+  return c;
+}
+
 // int3 high-bit word rotation per k-step (oracle/quant_oracle.py RHO3)
 __host__ __device__ constexpr int rho3(int s) { return s == 0 ? 0 : s == 1 ? 1 : s == 2 ? 8 : 9; }
 

@@ -3,32 +3,32 @@
 //
 // Replaces QuantLinear.forward -> F.linear(input, W_dq, bias) (quant/int_linear.py:48-65) on
 // packed weights.  HBM-bound: every weight byte is read exactly once, with one coalesced
-// 64 x (4*bits)-byte load per 16-row x 128-k tile and one 64-byte (scale, zero) load per tile and
-// group slot (qlin_common.h layout).
+// 64 x (4*bits)-byte non-temporal load per 16-row x 128-k tile and one 64-byte (scale, zero) load
+// per tile and group slot (qlin_common.h layout).
 //
 // Per wave, per k-step of 32: one v_and_or_b32 per code pair (+1 shift per word) turns the lane's
 // codes into the fp16 pairs (off_j + u_j); the default (exact) path then forms W_dq bit-exactly
 // ((off + u) - (off + z), times s: v_pk_add/v_pk_mul) — already the B operand of
 // v_mfma_f32_16x16x32_f16 — and the MFMA contracts it with x, so the result is the reference's
-// F.linear(x, W_dq) up to fp32 summation order.  x (A operand) is fetched per k-step straight from
-// L2 (16 B per lane; lanes whose A row is >= M re-read row M-1, whose C rows are never stored).
-// No LDS staging and no barrier precede the first MFMA.  (QLIN_GEMV_FAST=1 selects the variant
-// that feeds (off + u) directly and removes offsets / zero point / scale once per group with an
-// offset-column MFMA: ~5 VALU per 8 codes instead of ~13, at a ~3e-4 max-relative deviation from
-// F.linear(W_dq).)
+// F.linear(x, W_dq) up to fp32 summation order.  (Scale-after-accumulate variants that skip the
+// W_dq rounding save ~8 VALU per 8 codes but measured at most 5 % faster per launch and deviate
+// ~2e-4 of the output scale from F.linear(W_dq); not kept — DESIGN.md §4.)
 //
-// Every load is issued unconditionally from a wave-uniform base plus a per-lane offset and its
-// value is consumed only later, so hipcc keeps PF tiles in flight with counted vmcnt(N) waits; a
+// x (A operand): one 4*MT-byte load per lane per tile brings the tile's 128 k of all M rows
+// (64 lanes x 4*MT B); the wave parks it in its private LDS slot and reads the MFMA fragments
+// back with ds_read_b128 — 4x fewer vector-memory instructions than fetching each k-step's
+// fragment from L2 (measured -0.24 us per launch).
+//
+// Every global load is issued unconditionally from a wave-uniform base plus a per-lane offset
+// and consumed only later, so hipcc keeps PF tiles in flight with counted vmcnt(N) waits; a
 // "load or zero" select on a lane condition makes it wait vmcnt(0) at the join (measured: the
 // whole prefetch serialised).
 //
 // Decomposition: block = one 16-row tile row (grid = ceil(N/16)); its W <= 16 waves split K (tpw
-// tiles each, PF = 2 or 4 weight tiles in flight per wave) and combine their 16 x M partials
-// through LDS.
+// tiles each, PF = 2 or 4 tiles in flight per wave) and combine their 16 x M partials through
+// LDS.  Design measurements: tools/dev/gemv_lab.hip, DESIGN.md §4.
 #include "qlin_common.h"
 #include "../../include/qlin_gfx950.h"
-
-#include <stdlib.h>
 
 #include <type_traits>
 
@@ -44,51 +44,73 @@ struct WTile {
   uint32_t sz[GPT];  // packed (scale, zero) of each group slot, decoded only at use
 };
 
+// raw x words of one tile for MT rows: lane l holds 2*MT halfs of row l / (64/MT)
+template <int MT>
+struct XRaw {
+  uint32_t w[MT];
+};
+
 struct Geo {
   const uint32_t* qw_nt;  // this block's tile row of qweight (uniform)
   const uint32_t* sz_nt;  // this block's row tile of qsz (uniform)
-  const _Float16* x;
-  int K, G, group, gshift, lane, n_in, xoff;
+  const _Float16* xrow;   // x row this lane loads (row min(lane / (64/MT), M-1))
+  int K, G, group, lane, n_in, xk;  // xk: the lane's first k inside a tile
+  uint32_t gmagic;                   // ceil(2^31 / (group / 32)): branch-free k / group
 };
 
+// k / group for k, group multiples of 32 (k < 2^20): q = (k/32 * ceil(2^31/d)) >> 31 with
+// d = group/32 is exact because the rounding term stays below 1/d (d < 2^15)
 __device__ __forceinline__ int group_of(const Geo& g, int k) {
-  const int gi = g.gshift >= 0 ? (k >> g.gshift) : k / g.group;
+  const int gi = (int)(((uint64_t)(uint32_t)(k >> 5) * g.gmagic) >> 31);
   return min(gi, g.G - 1);
 }
 
 template <int BITS, int GPT>
 __device__ __forceinline__ void load_w(WTile<BITS, GPT>& t, const Geo& g, int kt) {
-  t.pc = load_piece<BITS>(g.qw_nt + kt * 64 * BITS + g.lane * BITS);
+  t.pc = load_piece_nt<BITS>(g.qw_nt + kt * 64 * BITS + g.lane * BITS);
 #pragma unroll
   for (int i = 0; i < GPT; ++i)
     t.sz[i] = g.sz_nt[group_of(g, kt * kTileK + 32 * (i * 4 / GPT)) * kTileN + g.n_in];
 }
 
-__device__ __forceinline__ void load_x(h8 (&xa)[4], const Geo& g, int kt) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int k = min(kt * kTileK + 32 * s, g.K - 32);  // uniform; + 8q + 7 stays < K
-    xa[s] = *reinterpret_cast<const h8*>(g.x + k + g.xoff);
+template <int MT>
+__device__ __forceinline__ void load_x(XRaw<MT>& r, const Geo& g, int kt) {
+  // k clamped into the row: lanes past K (last tile only) feed k-steps that are skipped
+  const int k = min(kt * kTileK + g.xk, g.K - 2 * MT);
+  const _Float16* p = g.xrow + k;
+  if constexpr (MT == 1) {
+    r.w[0] = *reinterpret_cast<const uint32_t*>(p);
+  } else if constexpr (MT == 2) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    r.w[0] = v.x; r.w[1] = v.y;
+  } else {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
   }
 }
 
-template <int BITS, int MT, int GPT, bool WIDE, bool EXACT, int PF>
-__device__ __forceinline__ void gemv_body(const Geo& g, int kt0, int nts, int ktl, f4& acc,
-                                          float (&yt)[4]) {
-  const Magics mg = make_magics<BITS>();
-  // fast path: offset column MFMA (column 0: off_k, column 1: 1) gives S1 = sum off x, S2 = sum x
-  f4 aoff = {0.f, 0.f, 0.f, 0.f};
-  h8 boff = {};
-  if constexpr (!EXACT) {
-#pragma unroll
-    for (int P = 0; P < 4; ++P) {
-      const _Float16 o = g.n_in == 0 ? (_Float16)pair_off<BITS>(P)
-                                     : g.n_in == 1 ? (_Float16)1.0f : (_Float16)0.0f;
-      boff[2 * P] = o;
-      boff[2 * P + 1] = o;
-    }
+// park a tile's x in the wave's LDS slot, read back the A fragments of its 4 k-steps:
+// lane (m = n_in, q) takes row min(m, MT-1) at k = 32s + 8q .. +7
+template <int MT>
+__device__ __forceinline__ void park_x(h8 (&xa)[4], const XRaw<MT>& r, uint32_t* slot, int lane,
+                                       int n_in) {
+  if constexpr (MT == 1) {
+    slot[lane] = r.w[0];
+  } else if constexpr (MT == 2) {
+    *reinterpret_cast<uint2*>(slot + 2 * lane) = make_uint2(r.w[0], r.w[1]);
+  } else {
+    *reinterpret_cast<uint4*>(slot + 4 * lane) = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
   }
-  int gend = (group_of(g, kt0 * kTileK) + 1) * g.group;  // k at which the current group ends
+  const int m = min(n_in, MT - 1);
+  const uint4* b = reinterpret_cast<const uint4*>(slot + 64 * m) + (lane >> 4);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, b[4 * s]);
+}
+
+template <int BITS, int MT, int GPT, bool WIDE, int PF>
+__device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0, int nts,
+                                          int ktl, f4& acc) {
+  const Magics mg = make_magics<BITS>();
 
   // FULL: the tile is not the matrix's last (only that one can hold fewer than 4 k-steps)
   auto step = [&](const WTile<BITS, GPT>& t, const h8 (&xa)[4], int kt, auto S_, auto FULL_) {
@@ -98,79 +120,61 @@ __device__ __forceinline__ void gemv_body(const Geo& g, int kt0, int nts, int kt
     const int k0 = kt * kTileK + 32 * S;
     if (FULL || k0 < g.K) {  // wave-uniform
       uint32_t v[4];
-      if constexpr (EXACT) {
-        const GroupQ gq = make_group<BITS, WIDE>(sz_scale(t.sz[slot]), sz_zero(t.sz[slot]));
-        dequant_step<BITS, WIDE, S>(t.pc, mg, gq, v);
-      } else {
-        step_pairs<BITS, S>(t.pc, mg, v);
-      }
+      const GroupQ gq = make_group<BITS, WIDE>(sz_scale(t.sz[slot]), sz_zero(t.sz[slot]));
+      dequant_step<BITS, WIDE, S>(t.pc, mg, gq, v);
       const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, acc, 0, 0, 0);
-      if constexpr (!EXACT) {
-        aoff = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], boff, aoff, 0, 0, 0);
-        if (k0 + 32 == gend) {  // group ends: y += s * (acc - S1 - z * S2)
-          const float sc = (float)sz_scale(t.sz[slot]), zf = (float)sz_zero(t.sz[slot]);
-#pragma unroll
-          for (int i = 0; i < MT && i < 4; ++i) {
-            // rows m < 4 live in lanes 0..15: column 0 holds S1_m, column 1 holds S2_m
-            const int ab = __builtin_bit_cast(int, aoff[i]);
-            const float s1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(ab, 0));
-            const float s2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(ab, 1));
-            yt[i] += sc * (acc[i] - (s1 + zf * s2));
-          }
-          acc = f4{0.f, 0.f, 0.f, 0.f};
-          aoff = f4{0.f, 0.f, 0.f, 0.f};
-          gend += g.group;
-        }
-      }
     }
   };
-  auto tile = [&](const WTile<BITS, GPT>& t, const h8 (&xa)[4], int kt, auto FULL_) {
+  auto tile = [&](const WTile<BITS, GPT>& t, const XRaw<MT>& xr, int kt, auto FULL_) {
+    h8 xa[4];
+    park_x<MT>(xa, xr, xslot, g.lane, g.n_in);
     step(t, xa, kt, std::integral_constant<int, 0>{}, FULL_);
     step(t, xa, kt, std::integral_constant<int, 1>{}, FULL_);
     step(t, xa, kt, std::integral_constant<int, 2>{}, FULL_);
     step(t, xa, kt, std::integral_constant<int, 3>{}, FULL_);
   };
 
-  // prologue: PF weight tiles and 2 x tiles in flight, tile index clamped to the wave's last
+  // prologue: PF tiles (codes, (scale, zero), x) in flight, tile index clamped to the wave's last
   WTile<BITS, GPT> wt[PF];
-  h8 xa[2][4];
-  load_x(xa[0], g, min(kt0, ktl));
-  load_w(wt[0], g, min(kt0, ktl));
-  load_w(wt[1], g, min(kt0 + 1, ktl));
-  load_x(xa[1], g, min(kt0 + 1, ktl));
+  XRaw<MT> xq[PF];
 #pragma unroll
-  for (int u = 2; u < PF; ++u) load_w(wt[u], g, min(kt0 + u, ktl));
+  for (int u = 0; u < PF; ++u) {
+    load_x<MT>(xq[u], g, min(kt0 + u, ktl));
+    load_w(wt[u], g, min(kt0 + u, ktl));
+  }
 
-  // full rounds of PF tiles: compute tile t, refill its x slot with t + 2, its weight slot with
-  // t + PF (invariant at the top of a round: wt[u] = tile t0 + u, xa[0/1] = tiles t0, t0 + 1)
+  // full rounds of PF tiles: compute tile t, refill its slot with tile t + PF
   int t0 = 0;
   for (; t0 + PF < nts; t0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int kt = kt0 + t0 + u;
-      tile(wt[u], xa[u & 1], kt, std::true_type{});
-      load_x(xa[u & 1], g, min(kt + 2, ktl));
+      tile(wt[u], xq[u], kt, std::true_type{});
+      load_x<MT>(xq[u], g, min(kt + PF, ktl));
       load_w(wt[u], g, min(kt + PF, ktl));
     }
   }
-  // last round (1..PF tiles): compute only, plus the x refills its tiles 2, 3 need
+  // last round (1..PF tiles): compute only; a tile short of K (the matrix's last) takes the
+  // per-k-step checks, every other one the straight-line body
 #pragma unroll
   for (int u = 0; u < PF; ++u) {
+    const int kt = kt0 + t0 + u;
     if (t0 + u < nts) {
-      const int kt = kt0 + t0 + u;
-      tile(wt[u], xa[u & 1], kt, std::false_type{});
-      if (u + 2 < PF) load_x(xa[u & 1], g, min(kt + 2, ktl));
+      if ((kt + 1) * kTileK <= g.K) tile(wt[u], xq[u], kt, std::true_type{});
+      else tile(wt[u], xq[u], kt, std::false_type{});
     }
   }
+
 }
 
-template <int BITS, int MT, int GPT, bool WIDE, bool EXACT, int PF>
+template <int BITS, int MT, int GPT, bool WIDE, int PF>
 __global__ __launch_bounds__(1024) void gemv_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
-    int M, int N, int K, int group, int gshift, int tpw) {
-  __shared__ float red[kMaxWaves * MT * kTileN];
+    int M, int N, int K, int group, uint32_t gmagic, int tpw) {
+  __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
+  __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
   const int W = blockDim.x >> 6;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
@@ -180,37 +184,40 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
   g.K = K;
   g.G = K / group;
   g.group = group;
-  g.gshift = gshift;
+  g.gmagic = gmagic;
   g.lane = tid & 63;
   g.n_in = g.lane & 15;
   g.qw_nt = qw + (int64_t)nt * Kt * 64 * BITS;
   g.sz_nt = qsz + (int64_t)nt * g.G * kTileN;
-  g.x = x;
-  // A operand: lane (m = n_in, q) supplies x row m at k = 32s + 8q + j
-  g.xoff = min(g.n_in, M - 1) * K + 8 * (g.lane >> 4);
+  constexpr int LPR = 64 / MT;  // lanes per x row
+  g.xrow = x + (int64_t)min(g.lane / LPR, M - 1) * K;
+  g.xk = 2 * MT * (g.lane % LPR);
   const int kt0 = wave * tpw;
   const int nts = max(0, min(tpw, Kt - kt0));
   const int ktl = max(0, min(Kt - 1, kt0 + nts - 1));
 
   f4 acc = {0.f, 0.f, 0.f, 0.f};
-  float yt[4] = {0.f, 0.f, 0.f, 0.f};
-  gemv_body<BITS, MT, GPT, WIDE, EXACT, PF>(g, kt0, nts, ktl, acc, yt);
-  if constexpr (EXACT) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) yt[i] = acc[i];
-  }
+  gemv_body<BITS, MT, GPT, WIDE, PF>(g, &xs[wave][0], kt0, nts, ktl, acc);
 
-  // combine the W partials of each (row m < MT, column n): C rows m < 4 live in lanes 0..15
+  // combine the W partials of each (row m < MT, column n): C rows m < 4 live in lanes 0..15;
+  // layout [m][n][wave] so one thread reads its 16 partials with 4 ds_read_b128
   if (g.lane < kTileN) {
 #pragma unroll
-    for (int i = 0; i < MT && i < 4; ++i) red[(wave * MT + i) * kTileN + g.n_in] = yt[i];
+    for (int i = 0; i < MT; ++i) red[(i * kTileN + g.n_in) * kMaxWaves + wave] = acc[i];
+    if (wave == 0) {
+      for (int w = W; w < kMaxWaves; ++w)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) red[(i * kTileN + g.n_in) * kMaxWaves + w] = 0.f;
+    }
   }
   __syncthreads();
   if (tid < MT * kTileN) {
     const int m = tid / kTileN, n = tid - m * kTileN;
     const int64_t row = (int64_t)nt * kTileN + n;
-    float t = 0.f;
-    for (int w = 0; w < W; ++w) t += red[(w * MT + m) * kTileN + n];
+    const f4* r = reinterpret_cast<const f4*>(red + tid * kMaxWaves);
+    const f4 a = r[0], b = r[1], c = r[2], d = r[3];
+    const f4 e = (a + b) + (c + d);
+    float t = (e[0] + e[1]) + (e[2] + e[3]);
     if (m < M && row < N) {
       if (bias) t += (float)bias[row];
       y[(int64_t)m * N + row] = (_Float16)t;
@@ -257,11 +264,9 @@ bool valid_layout(int64_t N, int64_t K, int bits, int group) {
          group % 32 == 0 && K % group == 0 && (bits == 2 || bits == 3 || bits == 4 || bits == 8);
 }
 
-int log2_or_neg(int v) {
-  if (v <= 0 || (v & (v - 1))) return -1;
-  int s = 0;
-  while ((1 << s) < v) ++s;
-  return s;
+uint32_t group_magic(int group) {
+  const uint64_t d = (uint64_t)(group / 32);
+  return (uint32_t)(((1ull << 31) + d - 1) / d);
 }
 
 // waves per block: grow W until the grid holds ~16 waves for each of the 256 CUs
@@ -273,38 +278,22 @@ int pick_waves(int Nt, int Kt, int& tpw) {
   return (Kt + tpw - 1) / tpw;
 }
 
-bool gemv_fast() {
-  static const int fast = [] {
-    const char* e = getenv("QLIN_GEMV_FAST");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return fast != 0;
-}
-
-template <int BITS, int MT, int GPT, bool WIDE, bool EXACT>
-int launch_gemv_e(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
+template <int BITS, int MT, int GPT, bool WIDE>
+int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
   const int Nt = (N + kTileN - 1) / kTileN;
   const int Kt = (K + kTileK - 1) / kTileK;
   int tpw = 0;
   const int W = pick_waves(Nt, Kt, tpw);
-  const int gs = log2_or_neg(group);
+  const uint32_t gs = group_magic(group);
 #define QLIN_GV(PF)                                                                        \
-  hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, WIDE, EXACT, PF>), dim3(Nt), dim3(64 * W), \
+  hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, WIDE, PF>), dim3(Nt), dim3(64 * W), \
                      0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias,             \
                      (_Float16*)y, M, N, K, group, gs, tpw)
   if (tpw <= 2) QLIN_GV(2);
   else QLIN_GV(4);
 #undef QLIN_GV
   return (int)hipGetLastError();
-}
-
-template <int BITS, int MT, int GPT, bool WIDE>
-int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
-  if (gemv_fast())
-    return launch_gemv_e<BITS, MT, GPT, WIDE, false>(qw, qsz, x, bias, y, M, N, K, group, st);
-  return launch_gemv_e<BITS, MT, GPT, WIDE, true>(qw, qsz, x, bias, y, M, N, K, group, st);
 }
 
 template <int BITS, int MT, bool WIDE>
@@ -361,8 +350,8 @@ extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int f
   if (N == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
   const int m = (int)M, n = (int)N, k = (int)K;
-#define QLIN_G(B)                                                                   \
-  return (flags & QLIN_WIDE_ZERO)                                                   \
+#define QLIN_G(B)                                                                         \
+  return (flags & QLIN_WIDE_ZERO)                                                         \
              ? launch_gemv_m<B, true>(qweight, qsz, x, bias, y, m, n, k, group, st) \
              : launch_gemv_m<B, false>(qweight, qsz, x, bias, y, m, n, k, group, st)
   switch (bits) {

@@ -152,15 +152,19 @@ def layer_act_quant(layer):
     return False
 
 
-@torch.no_grad()
-def window_nll(model, tokens):
-    """Σ NLL of one window exactly as main.py:136-146 (CE over the shifted logits, times seqlen)."""
-    logits = model(tokens)
+def nll_from_logits(logits, tokens):
+    """main.py:136-146: CE over the shifted logits (in the logits' dtype), times seqlen."""
     shift_logits = logits[:, :-1, :]
     shift_labels = tokens[:, 1:]
     loss = nn.functional.cross_entropy(shift_logits.reshape(-1, shift_logits.size(-1)),
                                        shift_labels.reshape(-1))
     return loss.float() * tokens.shape[1]
+
+
+@torch.no_grad()
+def window_nll(model, tokens):
+    """Σ NLL of one window exactly as main.py:136-146."""
+    return nll_from_logits(model(tokens), tokens)
 
 
 @torch.no_grad()

@@ -51,13 +51,13 @@ def timed(fn, reps=20, ring=R, streams=1):
 
 def st(): return torch.cuda.current_stream().cuda_stream
 
-def gemv_ring(M, hot=False):
+def gemv_ring(M, hot=False, extra=0):
     def f(part=0, nparts=1):
         sel = mats if part == 0 else mats[part - 1::nparts]
         for j, m in enumerate(sel):
             mm = mats[0] if hot else m
             y = ys[(j + part) % len(ys)]
-            rc = q.qlin_gemv_f16(mm[0].data_ptr(), mm[1].data_ptr(), mm[2], x.data_ptr(), None, y.data_ptr(), M, N, K, BITS, GRP, st())
+            rc = q.qlin_gemv_f16(mm[0].data_ptr(), mm[1].data_ptr(), mm[2] | extra, x.data_ptr(), None, y.data_ptr(), M, N, K, BITS, GRP, st())
             assert rc == 0, rc
     return f
 

@@ -22,7 +22,7 @@ for s in $STEPS; do
       timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
       rc=$?; echo "bench rc=$rc"; tail -3 "$OUT/bench.log"; ok_or_stop $rc bench ;;
     prof)
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
          -- python "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/prof.log" 2>&1)
       rc=$?; echo "prof rc=$rc"; tail -3 "$OUT/prof.log"; ok_or_stop $rc prof
       find "$OUT/prof" -name "*kernel_stats.csv" -exec head -20 {} \; ;;
