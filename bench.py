@@ -41,9 +41,11 @@ WORKLOADS = {
 }
 
 
-def algo_bytes(M, N, K, bits, group, zero_bytes=2):
-    """2MK + N*K*bits/8 + N*(K/g)*(2 + zb) + 2MN; the qsz layout stores each
-    group's fp16 scale and int16 zero point in one 32-bit word (zb = 2)."""
+def algo_bytes(M, N, K, bits, group, zero_bytes=1):
+    """Algorithmic bytes of one launch, SURVEY.md §8(d) / BASELINE.md §2:
+    2MK + N*K*bits/8 + N*(K/g)*(2 + zb) + 2MN with zb = 1 (fp16 scale + int8 zero per group).
+    The qsz layout actually stores an int16 zero (4 B per group, zero_bytes=2): reported as
+    bytes_read_per_launch beside it."""
     return 2 * M * K + N * K * bits // 8 + N * (K // group) * (2 + zero_bytes) + 2 * M * N
 
 
@@ -195,7 +197,8 @@ def main():
 
     launches = args.steps * R
     flops = 2.0 * M * N * K
-    nbytes = algo_bytes(M, N, K, bits, group, zb)
+    nbytes = algo_bytes(M, N, K, bits, group)
+    read_bytes = algo_bytes(M, N, K, bits, group, zb)
     per_launch_s = elapsed / launches
     value = flops * launches * world / elapsed / 1e12
     hbm_bound = kernel == "gemv" or M <= 256
@@ -208,6 +211,7 @@ def main():
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
     roof["traffic"] = None
     roof["bytes_per_launch"] = nbytes
+    roof["bytes_read_per_launch"] = read_bytes
     roof["us_per_launch"] = round(per_launch_s * 1e6, 3)
     roof["timing"] = ("HIP events over the timed region / launches (graph replay of the ring; "
                       "includes the inter-kernel dispatch gap)" if use_graph else
