@@ -33,7 +33,8 @@ WORKLOADS = {
                        "LLaMA3-8B int4 g128 dequant-GEMV batch=1 (configs[1]), 4096x4096"),
     "gemv_int3_g64": (1, 4096, 4096, 3, 64, 64, "gemv", "int3 g64 sub-byte GEMV (configs[3])"),
     "gemv_int2_g64": (1, 4096, 4096, 2, 64, 96, "gemv", "int2 g64 sub-byte GEMV (configs[3])"),
-    "gemm_int4_g128_m32": (32, 4096, 4096, 4, 128, 64, "gemm", "int4 g128, 32 tokens"),
+    "gemm_int4_g128_m32": (32, 4096, 4096, 4, 128, 64, "linear",
+                           "int4 g128, 32 tokens (qlin_linear_f16 dispatch: GEMV kernel x2)"),
     "gemm_int4_g128_m2048": (2048, 4096, 4096, 4, 128, 4, "gemm",
                              "int4 g128, one 2048-token PPL window"),
     "gemm_int4_g128_m65536": (65536, 4096, 4096, 4, 128, 1, "gemm",
@@ -139,13 +140,14 @@ def main():
     x = torch.empty(M, K, device=dev, dtype=torch.float16).normal_(0.0, 1.0, generator=gen)
     ys = [torch.empty(M, N, device=dev, dtype=torch.float16) for _ in range(min(R, 4))]
     lib = qlin.load_library()
-    fn = lib.qlin_gemv_f16 if kernel == "gemv" else lib.qlin_gemm_f16
+    fn = {"gemv": lib.qlin_gemv_f16, "linear": lib.qlin_linear_f16,
+          "gemm": lib.qlin_gemm_f16}[kernel]
 
     def step():
         st = torch.cuda.current_stream(dev).cuda_stream
         for i, (qw, qsz, fl) in enumerate(mats):
             y = ys[i % len(ys)]
-            if kernel == "gemv":
+            if kernel in ("gemv", "linear"):
                 rc = fn(qw.data_ptr(), qsz.data_ptr(), fl, x.data_ptr(), None,
                         y.data_ptr(), M, N, K, bits, group, st)
             else:
@@ -154,7 +156,7 @@ def main():
             if rc != 0:
                 raise RuntimeError(f"kernel failed: {rc}")
 
-    use_graph = not args.no_graph and kernel == "gemv"
+    use_graph = not args.no_graph and kernel in ("gemv", "linear")
 
     def make_runner():
         if not use_graph:
@@ -201,7 +203,7 @@ def main():
     read_bytes = algo_bytes(M, N, K, bits, group, zb)
     per_launch_s = elapsed / launches
     value = flops * launches * world / elapsed / 1e12
-    hbm_bound = kernel == "gemv" or M <= 256
+    hbm_bound = kernel in ("gemv", "linear") or M <= 256
     if hbm_bound:
         roof = {"bound": "hbm", "achieved": round(nbytes / per_launch_s / 1e9, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s"}
@@ -239,7 +241,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(M, N, K, bits, group, args.cpu_seconds) \
-            if kernel == "gemv" else cpu_baseline(min(M, 32), N, K, bits, group, args.cpu_seconds)
+            if kernel != "gemm" else cpu_baseline(min(M, 32), N, K, bits, group, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

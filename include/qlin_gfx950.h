@@ -112,9 +112,9 @@ int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, in
  * y[M, N] = x[M, K] @ W_dq[N, K]^T (+ bias[N]) with the group-wise unpack + dequant fused into the
  * product; fp16 in/out, fp32 accumulation.  Replaces QuantLinear.forward's
  * fwd_func(input, weight, bias) = F.linear (quant/int_linear.py:62) on packed weights.
- *   qlin_gemv_f16: matrix-core GEMV, 1 <= M <= 4 (decode).
+ *   qlin_gemv_f16: matrix-core GEMV, 1 <= M <= 16 (decode / small batches).
  *   qlin_gemm_f16: MFMA (v_mfma_f32_*_f16) tiles, any M >= 1 (prefill / PPL windows).
- *   qlin_linear_f16: picks one of the two from M.
+ *   qlin_linear_f16: picks from M: GEMV for M <= 64 (16-row chunks), MFMA GEMM above.
  *   workspace: reserved, pass NULL.
  */
 int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,

@@ -1,4 +1,4 @@
-// qlin_gemm.hip — fused dequant + MFMA GEMM for batched tokens (M > 4), gfx950.
+// qlin_gemm.hip — fused dequant + MFMA GEMM for batched tokens (M > 64 via qlin_linear_f16), gfx950.
 //
 // y[M, N] = x[M, K] @ W_dq[N, K]^T (+ bias): replaces F.linear at quant/int_linear.py:62 for the
 // prefill / PPL-window shapes (M = 2048 per window, main.py:127-136; M = 65,536 for batch 32).
@@ -19,6 +19,7 @@ using namespace qlin;
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int64_t kSkinnyMaxM = 64;  // qlin_linear_f16: M <= this runs the GEMV kernel
 constexpr int BM = 128, BN = 128, BK = kTileK;  // one k-tile of the packed layout per K-step
 constexpr int kRowBytes = BK * 2;                 // 256 B per LDS row = one LDS bank row
 
@@ -230,6 +231,16 @@ extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int
                                const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
                                int64_t N, int64_t K, int bits, int group, void* stream) {
   if (M == 0) return QLIN_OK;
-  if (M <= 4) return qlin_gemv_f16(qweight, qsz, flags, x, bias, y, M, N, K, bits, group, stream);
+  if (M <= kSkinnyMaxM) {
+    // skinny batches: the GEMV kernel in 16-row chunks (weights re-streamed per chunk, still far
+    // better parallelised than 128-row GEMM tiles for these M)
+    for (int64_t m0 = 0; m0 < M; m0 += 16) {
+      const int64_t mc = M - m0 < 16 ? M - m0 : 16;
+      const int rc = qlin_gemv_f16(qweight, qsz, flags, x + m0 * K, bias, y + m0 * N, mc, N, K,
+                                   bits, group, stream);
+      if (rc) return rc;
+    }
+    return QLIN_OK;
+  }
   return qlin_gemm_f16(qweight, qsz, flags, x, bias, y, M, N, K, bits, group, nullptr, stream);
 }

@@ -1,5 +1,5 @@
 // qlin_gemv.hip — fused unpack + group dequant + GEMV for decode-sized M (1..4) on the matrix
-// cores, gfx950, plus the standalone exact dequant kernel.
+// cores (M = 1..16: the A operand's 16 rows), gfx950, plus the standalone exact dequant kernel.
 //
 // Replaces QuantLinear.forward -> F.linear(input, W_dq, bias) (quant/int_linear.py:48-65) on
 // packed weights.  HBM-bound: every weight byte is read exactly once, with one coalesced
@@ -37,6 +37,7 @@ using namespace qlin;
 namespace {
 
 constexpr int kMaxWaves = 16;
+constexpr int kGemvMaxM = 16;  // one MFMA row block
 
 template <int BITS, int GPT>
 struct WTile {
@@ -84,13 +85,16 @@ __device__ __forceinline__ void load_x(XRaw<MT>& r, const Geo& g, int kt) {
     const uint2 v = *reinterpret_cast<const uint2*>(p);
     r.w[0] = v.x; r.w[1] = v.y;
   } else {
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
-    r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
+#pragma unroll
+    for (int c = 0; c < MT / 4; ++c) {
+      const uint4 v = reinterpret_cast<const uint4*>(p)[c];
+      r.w[4 * c] = v.x; r.w[4 * c + 1] = v.y; r.w[4 * c + 2] = v.z; r.w[4 * c + 3] = v.w;
+    }
   }
 }
 
-// park a tile's x in the wave's LDS slot, read back the A fragments of its 4 k-steps:
-// lane (m = n_in, q) takes row min(m, MT-1) at k = 32s + 8q .. +7
+// park a tile's x in the wave's LDS slot (row m at words 64m .. 64m+63), read back the A
+// fragments of its 4 k-steps: lane (m = n_in, q) takes row min(m, MT-1) at k = 32s + 8q .. +7
 template <int MT>
 __device__ __forceinline__ void park_x(h8 (&xa)[4], const XRaw<MT>& r, uint32_t* slot, int lane,
                                        int n_in) {
@@ -99,7 +103,10 @@ __device__ __forceinline__ void park_x(h8 (&xa)[4], const XRaw<MT>& r, uint32_t*
   } else if constexpr (MT == 2) {
     *reinterpret_cast<uint2*>(slot + 2 * lane) = make_uint2(r.w[0], r.w[1]);
   } else {
-    *reinterpret_cast<uint4*>(slot + 4 * lane) = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+#pragma unroll
+    for (int c = 0; c < MT / 4; ++c)
+      reinterpret_cast<uint4*>(slot + MT * lane)[c] =
+          make_uint4(r.w[4 * c], r.w[4 * c + 1], r.w[4 * c + 2], r.w[4 * c + 3]);
   }
   const int m = min(n_in, MT - 1);
   const uint4* b = reinterpret_cast<const uint4*>(slot + 64 * m) + (lane >> 4);
@@ -199,22 +206,27 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   gemv_body<BITS, MT, GPT, WIDE, PF>(g, &xs[wave][0], kt0, nts, ktl, acc);
 
-  // combine the W partials of each (row m < MT, column n): C rows m < 4 live in lanes 0..15;
-  // layout [m][n][wave] so one thread reads its 16 partials with 4 ds_read_b128
-  if (g.lane < kTileN) {
+  // combine the W partials of each (row m < MT, column n): C row m = 4q + i sits in lane
+  // n + 16q, element i; layout [m][n][wave] so one thread reads its 16 partials with 4
+  // ds_read_b128
+  const int q4 = 4 * (g.lane >> 4);
+  if (q4 < MT) {
 #pragma unroll
-    for (int i = 0; i < MT; ++i) red[(i * kTileN + g.n_in) * kMaxWaves + wave] = acc[i];
+    for (int i = 0; i < 4 && i < MT; ++i)
+      red[((q4 + i) * kTileN + g.n_in) * kMaxWaves + wave] = acc[i];
     if (wave == 0) {
       for (int w = W; w < kMaxWaves; ++w)
 #pragma unroll
-        for (int i = 0; i < MT; ++i) red[(i * kTileN + g.n_in) * kMaxWaves + w] = 0.f;
+        for (int i = 0; i < 4 && i < MT; ++i)
+          red[((q4 + i) * kTileN + g.n_in) * kMaxWaves + w] = 0.f;
     }
   }
   __syncthreads();
-  if (tid < MT * kTileN) {
-    const int m = tid / kTileN, n = tid - m * kTileN;
+  // MT * 16 outputs; a block of W < MT / 4 waves (short K) loops
+  for (int o = tid; o < MT * kTileN; o += blockDim.x) {
+    const int m = o / kTileN, n = o - m * kTileN;
     const int64_t row = (int64_t)nt * kTileN + n;
-    const f4* r = reinterpret_cast<const f4*>(red + tid * kMaxWaves);
+    const f4* r = reinterpret_cast<const f4*>(red + o * kMaxWaves);
     const f4 a = r[0], b = r[1], c = r[2], d = r[3];
     const f4 e = (a + b) + (c + d);
     float t = (e[0] + e[1]) + (e[2] + e[3]);
@@ -290,8 +302,12 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, WIDE, PF>), dim3(Nt), dim3(64 * W), \
                      0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias,             \
                      (_Float16*)y, M, N, K, group, gs, tpw)
-  if (tpw <= 2) QLIN_GV(2);
-  else QLIN_GV(4);
+  if constexpr (MT >= 8) {  // x registers of 4 tiles in flight would spill
+    QLIN_GV(2);
+  } else {
+    if (tpw <= 2) QLIN_GV(2);
+    else QLIN_GV(4);
+  }
 #undef QLIN_GV
   return (int)hipGetLastError();
 }
@@ -311,7 +327,9 @@ int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
   if (M == 1) return launch_gemv_g<BITS, 1, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
   if (M == 2) return launch_gemv_g<BITS, 2, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
-  return launch_gemv_g<BITS, 4, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (M <= 4) return launch_gemv_g<BITS, 4, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (M <= 8) return launch_gemv_g<BITS, 8, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  return launch_gemv_g<BITS, 16, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
 }
 
 }  // namespace
@@ -345,7 +363,7 @@ extern "C" int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, in
 extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                              const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
                              int64_t N, int64_t K, int bits, int group, void* stream) {
-  if (!qweight || !qsz || !x || !y || M < 1 || M > 4 || !valid_layout(N, K, bits, group))
+  if (!qweight || !qsz || !x || !y || M < 1 || M > kGemvMaxM || !valid_layout(N, K, bits, group))
     return QLIN_EINVAL;
   if (N == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;

@@ -250,7 +250,8 @@ def _linear_call(fn_name, x, qweight, qsz, bias, N, K, bits, group, flags, extra
 
 
 def linear(x, qweight, qsz, bias, N, K, bits, group, flags=0):
-    """Dispatching fused dequant-matmul (GEMV for M <= 4, MFMA GEMM otherwise)."""
+    """Dispatching fused dequant-matmul (GEMV kernel for M <= 64 in 16-row chunks, MFMA GEMM
+    above)."""
     return _linear_call("qlin_linear_f16", x, qweight, qsz, bias, N, K, bits, group, flags)
 
 

@@ -123,7 +123,7 @@ def test_gemv_matches_oracle(bits, shape):
         group = 64 if K % 64 == 0 else group
     qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=N + K + bits)
     bias = np.random.RandomState(3).randn(N).astype(np.float16) * np.float16(0.1)
-    for M in (1, 2, 3, 4):
+    for M in (1, 2, 3, 4, 5, 8, 13, 16):
         x = rand_x(M, K, seed=M)
         for b in (None, bias):
             y = qlin.gemv(t(x), qw, qsz, None if b is None else t(b), N, K, bits, group, fl)
@@ -166,7 +166,8 @@ def test_gemm_matches_oracle(bits, shape):
 def test_linear_dispatch_and_batch_shapes():
     N, K, group = 384, 1024, 128
     qw, qsz, fl, wdq = _packed(N, K, 4, group, seed=11)
-    for shp in ((1, 1, K), (1, 3, K), (2, 5, K), (1, 64, K)):
+    for shp in ((1, 1, K), (1, 3, K), (2, 5, K), (1, 16, K), (1, 20, K), (2, 33, K), (1, 64, K),
+                (1, 65, K), (3, 50, K)):
         x = np.random.RandomState(len(shp)).randn(*shp).astype(np.float16)
         y = qlin.linear(t(x), qw, qsz, None, N, K, 4, group, fl)
         assert tuple(y.shape) == shp[:-1] + (N,)
@@ -189,6 +190,6 @@ def test_invalid_arguments_raise():
     y = torch.empty(1, N, dtype=torch.float16, device="cuda")
     # raw C ABI: M out of the GEMV range, null pointers
     assert lib.qlin_gemv_f16(qw.data_ptr(), qsz.data_ptr(), 0, x.data_ptr(), None, y.data_ptr(),
-                             5, N, K, 4, group, None) == 1
+                             17, N, K, 4, group, None) == 1
     assert lib.qlin_gemm_f16(None, qsz.data_ptr(), 0, x.data_ptr(), None, y.data_ptr(),
                              1, N, K, 4, group, None, None) == 1

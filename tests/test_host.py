@@ -48,7 +48,7 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert lib.qlin_pack_f16(None, None, None, 4, 64, 4, 64, 0, None, None, None) == 1
     p = ctypes.c_void_p(16)  # never dereferenced: the shape check fails first
     assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 1, 16, 65, 4, 64, None) == 1   # K % 32
-    assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 9, 16, 64, 4, 64, None) == 1   # M > 4
+    assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 17, 16, 64, 4, 64, None) == 1  # M > 16
     assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 1, 16, 64, 5, 64, None) == 1   # bits
     assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 1, 16, 128, 4, 96, None) == 1  # group | K
     assert lib.qlin_gemm_f16(p, p, 0, p, None, p, 8, 16, 64, 4, 48, None, None) == 1  # group % 32
