@@ -1,192 +1,292 @@
-// qlin_gemm.hip — fused dequant + MFMA GEMM for batched tokens (M > 64 via qlin_linear_f16), gfx950.
+// qlin_gemm.hip — fused dequant + MFMA GEMM for batched tokens (M > 64 via qlin_linear_f16),
+// gfx950.
 //
 // y[M, N] = x[M, K] @ W_dq[N, K]^T (+ bias): replaces F.linear at quant/int_linear.py:62 for the
 // prefill / PPL-window shapes (M = 2048 per window, main.py:127-136; M = 65,536 for batch 32).
 //
-// v1 structure (one 256-thread block = 4 waves in a 2x2 grid, block tile 128(M) x 128(N), BK = 128
-// = one k-tile of the packed layout):
-//   - A = x tile [128][128] fp16 and B = W tile [128][128] fp16 live in LDS with the 16-byte piece
-//     index XOR-swizzled by (row & 15) so a 32-row fragment read is bank-conflict-free;
-//   - each thread stages two lane pieces of the 8 packed row tiles (coalesced 1 KB per wave),
-//     dequantizes them bit-exactly (qlin_common.h) and writes 4 x 16 B of fp16 per piece;
-//   - the next K-step's global loads are issued before this step's MFMAs (register prefetch);
-//   - each wave computes a 64x64 sub-tile as 2x2 v_mfma_f32_32x32x16_f16 accumulators.
+// Structure (256-thread block = 4 waves, block tile 128 x 512 (int8: 128 x 256), wave tile 128 x 128
+// (int8: 64 x 128), BK = 128 = one packed k-tile, two LDS stages; wide-in-N waves because B is
+// read packed, 4x cheaper per LDS byte than A):
+//   - every operand reaches LDS by LDS-DMA (global_load_lds, 16 B per lane): the x tile (BM rows x
+//     256 B, XOR-swizzled per 16-B chunk by (row & 15) through the per-lane SOURCE address, so the
+//     LDS image stays lane-linear per instruction), the packed codes of the 8 row tiles (already
+//     lane-linear in the qlin tiled layout) and their (scale, zero) words;
+//   - B stays PACKED in LDS (bits/16 of the fp16 bytes): each wave reads the lane pieces of its 8
+//     row tiles once per k-tile and dequantizes them bit-exactly in registers (qlin_common.h) into
+//     the B operand of v_mfma_f32_16x16x32_f16 — the piece layout IS that operand, so no shuffle
+//     and no fp16 B image exist;
+//   - A fragments: ds_read_b128 of row (lane & 15), chunk (4s + q) ^ (row & 15): conflict-free,
+//     the next k-step's fragments read while this step's MFMAs run;
+//   - the next k-tile's DMA is issued right after the barrier and runs under this tile's MFMAs;
+//   - blocks are remapped so each XCD owns a contiguous band of M tiles (x re-use in its L2).
 #include "qlin_common.h"
 #include "../../include/qlin_gfx950.h"
+
+#include <type_traits>
 
 using namespace qlin;
 
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int64_t kSkinnyMaxM = 64;  // qlin_linear_f16: M <= this runs the GEMV kernel
-constexpr int BM = 128, BN = 128, BK = kTileK;  // one k-tile of the packed layout per K-step
-constexpr int kRowBytes = BK * 2;                 // 256 B per LDS row = one LDS bank row
+constexpr int BM = 128, BK = kTileK;  // block rows; one packed k-tile per stage
+constexpr int64_t kSkinnyMaxM = 64;   // qlin_linear_f16: M <= this runs the GEMV kernel
 
-// byte offset of 16-B piece c (0..15) of LDS row r: piece index XOR (r & 15) spreads the 16 rows
-// read by a ds_read_b128 lane group over all 16 bank slots (conflict-free)
-__device__ __forceinline__ int swz(int r, int c) { return r * kRowBytes + 16 * (c ^ (r & 15)); }
+typedef __attribute__((address_space(3))) void* lds_ptr;
+typedef __attribute__((address_space(1))) void* gbl_ptr;
 
-// the two lane pieces a thread stages per K-step: pieces tid and tid + 256 of the 8 row tiles
-template <int BITS, int GPT>
-struct BStage {
-  Piece<BITS> c[2];
-  uint32_t sz[2][GPT];  // packed (scale, zero) words, decoded at use
+// Wave tiles are 128 (or 64) rows x 128 columns: 8 B fragments dequantized per k-step feed
+// MB x 8 MFMAs, so the 13 VALU per fragment fit the issue slots the MFMAs leave free.
+// WIDE_N: block 128 x 512, 4 waves side by side in N (each B element dequantized once; 1.3x the
+// MFMA rate of the narrow tile at M >= 8192) — int2/3/4 when the grid has >= 2 blocks per CU;
+// otherwise block 128 x 256, waves 2 x 2 (twice the blocks; int8 always: twice the code bytes).
+template <int BITS, bool WIDE_N> struct Cfg {
+  static constexpr int BN = WIDE_N ? 512 : 256;
+  static constexpr int WGN = BN / 128, WGM = 4 / WGN;  // waves along N, along M
+  static constexpr int WM = BM / WGM, WN = 128;
+  static constexpr int MB = WM / 16, NB = WN / kTileN;  // 16 x 16 MFMA blocks per wave
+  static constexpr int RT = BN / kTileN;                // packed row tiles per block
+  static constexpr int A_BYTES = BM * BK * 2;           // 32 KB
+  static constexpr int B_BYTES = RT * 256 * BITS;       // packed codes
+  static constexpr int SZ_BYTES = RT * 4 * 64;          // up to 4 group slots per k-tile
+  static constexpr int STAGE = A_BYTES + B_BYTES + SZ_BYTES;
 };
 
-template <int BITS, int GPT>
-__device__ __forceinline__ void load_b(BStage<BITS, GPT>& b, const uint32_t* __restrict__ qw,
-                                       const uint32_t* __restrict__ qsz, int64_t nt0, int kt,
-                                       int Kt, int N, int K, int group, int tid) {
-  const int G = K / group;
-  const int64_t ntl = (N + kTileN - 1) / kTileN - 1;  // last row tile that exists
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr)g, (lds_ptr)lds, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* g, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr)g, (lds_ptr)lds, 4, 0, 0);
+}
+
+struct GemmGeo {
+  int64_t M;
+  int N, K, Kt, G, group, wave, lane;
+  uint32_t gmagic;
+  int64_t m0, nt0, ntl;
+};
+
+// k / group, branch-free (see qlin_gemv.hip group_of)
+__device__ __forceinline__ int gemm_group_of(const GemmGeo& g, int k) {
+  const int gi = (int)(((uint64_t)(uint32_t)(k >> 5) * g.gmagic) >> 31);
+  return min(gi, g.G - 1);
+}
+
+// one k-tile's DMA into stage buffer `st`: x tile, packed codes, (scale, zero) words
+template <int BITS, bool WN_, int GPT>
+__device__ __forceinline__ void load_stage(unsigned char* st, const GemmGeo& g, int kt,
+                                           const _Float16* __restrict__ x,
+                                           const uint32_t* __restrict__ qw,
+                                           const uint32_t* __restrict__ qsz) {
+  using C = Cfg<BITS, WN_>;
+  // x: BM rows x 16 chunks; one instruction = 4 rows (1 KB); wave w owns rows [BM/4 w, +BM/4).
+  // Rows >= M re-read row M-1 and k >= K re-reads the row's last chunk: those C rows are never
+  // stored and those k-steps are skipped.
+  {
+    const int sub = g.lane >> 4, p = g.lane & 15;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int p = tid + kThreads * h;
-    const int rt = p >> 6, lane = p & 63;
-    const int64_t nt = min(nt0 + rt, ntl);
-    b.c[h] = load_piece<BITS>(qw + piece_off(nt, kt, Kt, lane, BITS));
+    for (int j = 0; j < BM / 16; ++j) {
+      const int r = (BM / 4) * g.wave + 4 * j + sub;  // LDS row
+      const int c = p ^ (r & 15);                      // logical chunk held at physical p
+      const int64_t m = min(g.m0 + r, g.M - 1);
+      const int k = min(kt * BK + 8 * c, g.K - 8);
+      glds16(x + m * g.K + k, st + ((BM / 4) * g.wave + 4 * j) * 256);
+    }
+  }
+  // packed codes: RT row tiles x 256*BITS bytes, lane-linear 16-B chunks
+  {
+    constexpr int CH = C::RT * 16 * BITS;  // chunks per stage
+    unsigned char* bs = st + C::A_BYTES;
 #pragma unroll
-    for (int i = 0; i < GPT; ++i) {
-      const int g = min((kt * kTileK + 32 * (i * 4 / GPT)) / group, G - 1);
-      b.sz[h][i] = qsz[sz_index(nt, g, G, lane & 15)];
+    for (int j = g.wave; j < CH / 64; j += 4) {
+      const int c = 64 * j + g.lane;
+      const int rt = c / (16 * BITS), o = c % (16 * BITS);
+      const int64_t nt = min(g.nt0 + rt, g.ntl);
+      glds16(qw + ((nt * g.Kt + kt) * 64 * BITS + 4 * o), bs + 1024 * j);
+    }
+  }
+  // (scale, zero) words: [row tile][slot][16], 4 B per lane
+  {
+    unsigned char* ss = st + C::A_BYTES + C::B_BYTES;
+    constexpr int WORDS = C::RT * GPT * 16;
+#pragma unroll
+    for (int j = g.wave; j < WORDS / 64; j += 4) {
+      const int w = 64 * j + g.lane;
+      const int rt = w / (16 * GPT), i = (w / 16) % GPT, n = w & 15;
+      const int64_t nt = min(g.nt0 + rt, g.ntl);
+      const int gi = gemm_group_of(g, kt * BK + 32 * (i * 4 / GPT));
+      glds4(qsz + sz_index(nt, gi, g.G, n), ss + 256 * j);
     }
   }
 }
 
-template <int BITS, int GPT, bool WIDE>
-__device__ __forceinline__ void store_b(unsigned char* sB, const BStage<BITS, GPT>& b, int kt,
-                                        int K, int tid) {
+// A fragments of k-step S for the wave's MB row blocks: row (lane & 15), chunk (4S + q) ^ (row & 15)
+template <int S, int MB, int WM>
+__device__ __forceinline__ void read_a(h8 (&a)[MB], const unsigned char* as, int wm, int n_in,
+                                       int q) {
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int r = wm * WM + mb * 16 + n_in;
+    const int c = (4 * S + q) ^ (r & 15);
+    a[mb] = *reinterpret_cast<const h8*>(as + r * 256 + c * 16);
+  }
+}
+
+template <int BITS, bool WN_, int GPT, bool WIDE>
+__device__ __forceinline__ void compute_stage(const unsigned char* st, const GemmGeo& g, int kt,
+                                              f4 (&acc)[Cfg<BITS, WN_>::MB][Cfg<BITS, WN_>::NB]) {
+  using C = Cfg<BITS, WN_>;
+  constexpr int MB = C::MB, NB = C::NB, WM = C::WM;
+  const int wm = g.wave / C::WGN, wn = g.wave % C::WGN;
+  const int lane = g.lane, n_in = lane & 15, q = lane >> 4;
+  const unsigned char* as = st;
+  const uint32_t* bs = reinterpret_cast<const uint32_t*>(st + C::A_BYTES);
+  const uint32_t* ss = reinterpret_cast<const uint32_t*>(st + C::A_BYTES + C::B_BYTES);
   const Magics mg = make_magics<BITS>();
+  // the wave's 8 lane pieces; int8 pieces (32 B) are read per half (steps 0-1, then 2-3)
+  constexpr int PW = BITS == 8 ? 4 : BITS;  // words held per piece at a time
+  Piece<BITS> pc[NB];
+  auto read_pieces = [&](int half) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int p = tid + kThreads * h;
-    const int rt = p >> 6, lane = p & 63;
-    const int r = rt * kTileN + (lane & 15), q = lane >> 4;
-    auto one = [&](auto S_) {
-      constexpr int S = decltype(S_)::value;
-      uint32_t o[4] = {0u, 0u, 0u, 0u};
-      if (kt * kTileK + 32 * S < K) {
-        constexpr int slot = S * GPT / 4;
-        const GroupQ g = make_group<BITS, WIDE>(sz_scale(b.sz[h][slot]), sz_zero(b.sz[h][slot]));
-        dequant_step<BITS, WIDE, S>(b.c[h], mg, g, o);
+    for (int nb = 0; nb < NB; ++nb) {
+      const uint32_t* p = bs + (wn * NB + nb) * 64 * BITS + lane * BITS + half * PW;
+      if constexpr (BITS == 8) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        pc[nb].w[4 * half] = v.x; pc[nb].w[4 * half + 1] = v.y;
+        pc[nb].w[4 * half + 2] = v.z; pc[nb].w[4 * half + 3] = v.w;
+      } else {
+        pc[nb] = load_piece<BITS>(p);
       }
-      *reinterpret_cast<uint4*>(sB + swz(r, 4 * S + q)) = make_uint4(o[0], o[1], o[2], o[3]);
-    };
-    one(std::integral_constant<int, 0>{});
-    one(std::integral_constant<int, 1>{});
-    one(std::integral_constant<int, 2>{});
-    one(std::integral_constant<int, 3>{});
-  }
-}
-
-// x tile [128 rows][128 k]: 2048 16-B pieces, 8 per thread; k >= K and m >= M read as zero
-__device__ __forceinline__ void load_a(uint4 (&a)[8], const _Float16* __restrict__ x, int64_t m0,
-                                       int64_t M, int k0, int K, int tid) {
+    }
+  };
+  GroupQ gq[NB];
+  auto read_groups = [&](int slot) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int p = tid + kThreads * i;
-    const int r = p >> 4, c = p & 15;
-    const int64_t m = m0 + r;
-    const int k = k0 + 8 * c;
-    a[i] = (m < M && k < K) ? *reinterpret_cast<const uint4*>(x + m * K + k) : make_uint4(0, 0, 0, 0);
-  }
-}
+    for (int nb = 0; nb < NB; ++nb) {
+      const uint32_t sw = ss[((wn * NB + nb) * GPT + slot) * 16 + n_in];
+      gq[nb] = make_group<BITS, WIDE>(sz_scale(sw), sz_zero(sw));
+    }
+  };
 
-__device__ __forceinline__ void store_a(unsigned char* sA, const uint4 (&a)[8], int tid) {
+  h8 a[2][MB];
+  read_pieces(0);
+  read_a<0, MB, WM>(a[0], as, wm, n_in, q);
+  auto step = [&](auto S_) {
+    constexpr int S = decltype(S_)::value;
+    if constexpr (S * GPT / 4 != (S - 1) * GPT / 4 || S == 0) read_groups(S * GPT / 4);
+    if constexpr (BITS == 8 && S == 2) read_pieces(1);
+    if constexpr (S < 3) read_a<S + 1, MB, WM>(a[(S + 1) & 1], as, wm, n_in, q);  // next A in flight
+    if (kt * BK + 32 * S >= g.K) return;  // wave-uniform: only the last k-tile can be short
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int p = tid + kThreads * i;
-    *reinterpret_cast<uint4*>(sA + swz(p >> 4, p & 15)) = a[i];
-  }
+    for (int nb = 0; nb < NB; ++nb) {
+      uint32_t v[4];
+      dequant_step<BITS, WIDE, S>(pc[nb], mg, gq[nb], v);
+      const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[S & 1][mb], b, acc[mb][nb], 0, 0, 0);
+    }
+  };
+  step(std::integral_constant<int, 0>{});
+  step(std::integral_constant<int, 1>{});
+  step(std::integral_constant<int, 2>{});
+  step(std::integral_constant<int, 3>{});
 }
 
-template <int BITS, int GPT, bool WIDE>
+// ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
+// the DMA after the first k-tile; the library instantiates ABL = 0 only
+template <int BITS, bool WN_, int GPT, bool WIDE, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
-    int64_t M, int N, int K, int group, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BM * kRowBytes];
-  unsigned char* sA = smem;
-  unsigned char* sB = smem + BM * kRowBytes;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  // n-tile fastest: consecutive blocks share the x tile in L2
-  const int64_t tile_m = blockIdx.x / tiles_n;
-  const int tile_n = blockIdx.x - (int)(tile_m * tiles_n);
-  const int64_t m0 = tile_m * BM;
-  const int64_t nt0 = (int64_t)tile_n * (BN / kTileN);
-  const int Kt = (K + kTileK - 1) / kTileK;
+    int64_t M, int N, int K, int group, uint32_t gmagic, int tiles_m, int tiles_n) {
+  using C = Cfg<BITS, WN_>;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * C::STAGE];
+  GemmGeo g;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.Kt = (K + BK - 1) / BK;
+  g.G = K / group;
+  g.group = group;
+  g.gmagic = gmagic;
+  g.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  g.lane = threadIdx.x & 63;
+  // XCD-aware order: dispatch puts block b on XCD b % 8; give each XCD a contiguous run of
+  // (tile_m, tile_n) with n fastest so its blocks share x tiles in that XCD's L2
+  const int nblk = tiles_m * tiles_n;
+  const int b = blockIdx.x;
+  int lb = b;
+  if ((nblk & 7) == 0) lb = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int tile_m = lb / tiles_n, tile_n = lb - tile_m * tiles_n;
+  g.m0 = (int64_t)tile_m * BM;
+  g.nt0 = (int64_t)tile_n * C::RT;
+  g.ntl = (N + kTileN - 1) / kTileN - 1;
 
-  f16v acc[2][2];
+  f4 acc[C::MB][C::NB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < C::MB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    for (int j = 0; j < C::NB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 a[8];
-  BStage<BITS, GPT> b;
-  load_a(a, x, m0, M, 0, K, tid);
-  load_b<BITS, GPT>(b, qw, qsz, nt0, 0, Kt, N, K, group, tid);
-
-  const int r32 = lane & 31, h = lane >> 5;
-  for (int kt = 0; kt < Kt; ++kt) {
+  load_stage<BITS, WN_, GPT>(smem, g, 0, x, qw, qsz);
+  for (int kt = 0; kt < g.Kt; ++kt) {
+    // stage kt has landed for every wave, and every wave is done reading stage kt - 1
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
     __syncthreads();
-    store_a(sA, a, tid);
-    store_b<BITS, GPT, WIDE>(sB, b, kt, K, tid);
-    __syncthreads();
-    if (kt + 1 < Kt) {
-      load_a(a, x, m0, M, (kt + 1) * BK, K, tid);
-      load_b<BITS, GPT>(b, qw, qsz, nt0, kt + 1, Kt, N, K, group, tid);
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK / 16; ++kk) {
-      h8 af[2], bf[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        af[i] = *reinterpret_cast<const h8*>(sA + swz(wm * 64 + i * 32 + r32, kk * 2 + h));
-        bf[i] = *reinterpret_cast<const h8*>(sB + swz(wn * 64 + i * 32 + r32, kk * 2 + h));
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
+    if (!(ABL & 2) && kt + 1 < g.Kt)
+      load_stage<BITS, WN_, GPT>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
+    if (!(ABL & 1)) compute_stage<BITS, WN_, GPT, WIDE>(smem + (kt & 1) * C::STAGE, g, kt, acc);
   }
 
-  // epilogue: C/D layout col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
+  // epilogue: lane (n, q) holds C[4q + i][n] of each 16 x 16 block
+  const int wm = g.wave / C::WGN, wn = g.wave % C::WGN;
+  const int n_in = g.lane & 15, q = g.lane >> 4;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t n = nt0 * kTileN + wn * 64 + j * 32 + r32;
+  for (int nb = 0; nb < C::NB; ++nb) {
+    const int64_t n = (g.nt0 + wn * C::NB + nb) * kTileN + n_in;
     if (n >= N) continue;
     const float bv = bias ? (float)bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int mb = 0; mb < C::MB; ++mb) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int64_t m = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (m < M) y[m * N + n] = (_Float16)(acc[i][j][e] + bv);
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = g.m0 + wm * C::WM + mb * 16 + 4 * q + i;
+        if (m < M) y[m * N + n] = (_Float16)(acc[mb][nb][i] + bv);
       }
     }
   }
 }
+
+uint32_t group_magic(int group) {
+  const uint64_t d = (uint64_t)(group / 32);
+  return (uint32_t)(((1ull << 31) + d - 1) / d);
+}
+
+template <int BITS, bool WN_, int GPT, bool WIDE>
+int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
+                  uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
+  const int tiles_n = (N + Cfg<BITS, WN_>::BN - 1) / Cfg<BITS, WN_>::BN;
+  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t blocks = tiles_m * tiles_n;
+  if (blocks > 0x7fffffff) return QLIN_EINVAL;
+  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, WIDE>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                     st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, (_Float16*)y, M, N, K,
+                     group, group_magic(group), (int)tiles_m, tiles_n);
+  return (int)hipGetLastError();
+}
+
+constexpr int64_t kWideMinBlocks = 512;  // >= 2 blocks per CU on 256 CUs
 
 template <int BITS, int GPT, bool WIDE>
 int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                 uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
-  const int tiles_n = (N + BN - 1) / BN;
-  const int64_t tiles_m = (M + BM - 1) / BM;
-  const int64_t blocks = tiles_m * tiles_n;
-  if (blocks > 0x7fffffff) return QLIN_EINVAL;
-  hipLaunchKernelGGL((gemm_kernel<BITS, GPT, WIDE>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
-                     qw, qsz, (const _Float16*)x, (const _Float16*)bias, (_Float16*)y, M, N, K,
-                     group, tiles_n);
-  return (int)hipGetLastError();
+  if constexpr (BITS != 8) {
+    const int64_t wide_blocks = ((M + BM - 1) / BM) * ((N + 511) / 512);
+    if (wide_blocks >= kWideMinBlocks)
+      return launch_gemm_t<BITS, true, GPT, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  }
+  return launch_gemm_t<BITS, false, GPT, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
 }
 
 template <int BITS, bool WIDE>
@@ -198,8 +298,8 @@ int launch_gemm_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
 }
 
 bool valid(int64_t M, int64_t N, int64_t K, int bits, int group) {
-  return M >= 0 && N >= 0 && N <= (1 << 30) && K > 0 && K % 32 == 0 && K <= (1 << 20) &&
-         group > 0 && group % 32 == 0 && K % group == 0 &&
+  return M >= 0 && M <= (1ll << 40) && N >= 0 && N <= (1 << 30) && K > 0 && K % 32 == 0 &&
+         K <= (1 << 20) && group > 0 && group % 32 == 0 && K % group == 0 &&
          (bits == 2 || bits == 3 || bits == 4 || bits == 8);
 }
 
@@ -233,7 +333,7 @@ extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int
   if (M == 0) return QLIN_OK;
   if (M <= kSkinnyMaxM) {
     // skinny batches: the GEMV kernel in 16-row chunks (weights re-streamed per chunk, still far
-    // better parallelised than 128-row GEMM tiles for these M)
+    // better parallelised than the GEMM's 256-row tiles for these M)
     for (int64_t m0 = 0; m0 < M; m0 += 16) {
       const int64_t mc = M - m0 < 16 ? M - m0 : 16;
       const int rc = qlin_gemv_f16(qweight, qsz, flags, x + m0 * K, bias, y + m0 * N, mc, N, K,
