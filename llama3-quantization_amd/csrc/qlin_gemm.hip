@@ -132,7 +132,8 @@ __device__ __forceinline__ void read_a(h8 (&a)[MB], const unsigned char* as, int
   }
 }
 
-template <int BITS, bool WN_, int GPT, bool WIDE>
+// FULL: every k-tile lies inside K (K % 128 == 0, chosen per launch): straight-line k-steps
+template <int BITS, bool WN_, int GPT, bool WIDE, bool FULL>
 __device__ __forceinline__ void compute_stage(const unsigned char* st, const GemmGeo& g, int kt,
                                               f4 (&acc)[Cfg<BITS, WN_>::MB][Cfg<BITS, WN_>::NB]) {
   using C = Cfg<BITS, WN_>;
@@ -176,7 +177,7 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
     if constexpr (S * GPT / 4 != (S - 1) * GPT / 4 || S == 0) read_groups(S * GPT / 4);
     if constexpr (BITS == 8 && S == 2) read_pieces(1);
     if constexpr (S < 3) read_a<S + 1, MB, WM>(a[(S + 1) & 1], as, wm, n_in, q);  // next A in flight
-    if (kt * BK + 32 * S >= g.K) return;  // wave-uniform: only the last k-tile can be short
+    if (!FULL && kt * BK + 32 * S >= g.K) return;  // wave-uniform
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       uint32_t v[4];
@@ -195,7 +196,7 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 
 // ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
 // the DMA after the first k-tile; the library instantiates ABL = 0 only
-template <int BITS, bool WN_, int GPT, bool WIDE, int ABL = 0>
+template <int BITS, bool WN_, int GPT, bool WIDE, bool KFULL, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
@@ -236,7 +237,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(
     __syncthreads();
     if (!(ABL & 2) && kt + 1 < g.Kt)
       load_stage<BITS, WN_, GPT>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
-    if (!(ABL & 1)) compute_stage<BITS, WN_, GPT, WIDE>(smem + (kt & 1) * C::STAGE, g, kt, acc);
+    if (!(ABL & 1))
+      compute_stage<BITS, WN_, GPT, WIDE, KFULL>(smem + (kt & 1) * C::STAGE, g, kt, acc);
   }
 
   // epilogue: lane (n, q) holds C[4q + i][n] of each 16 x 16 block
@@ -270,9 +272,15 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   const int64_t tiles_m = (M + BM - 1) / BM;
   const int64_t blocks = tiles_m * tiles_n;
   if (blocks > 0x7fffffff) return QLIN_EINVAL;
-  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, WIDE>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                     st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, (_Float16*)y, M, N, K,
-                     group, group_magic(group), (int)tiles_m, tiles_n);
+#define QLIN_GL(KF)                                                                           \
+  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, WIDE, KF>), dim3((unsigned)blocks),           \
+                     dim3(kThreads), 0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, \
+                     (_Float16*)y, M, N, K, group, group_magic(group), (int)tiles_m, tiles_n)
+  // straight-line k-steps need K % 128 == 0; the wide tile with 2-4 group slots per k-tile then
+  // spills (the per-step checks bound the scheduler), so it keeps the checked form
+  if (K % BK == 0 && !(WN_ && GPT > 1)) QLIN_GL(true);
+  else QLIN_GL(false);
+#undef QLIN_GL
   return (int)hipGetLastError();
 }
 

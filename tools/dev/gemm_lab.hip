@@ -9,7 +9,7 @@ extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
   const int tiles_m = (int)((M + BM - 1) / BM);
   const dim3 grid(tiles_m * tiles_n);
 #define L(W, A)                                                                                 \
-  hipLaunchKernelGGL((gemm_kernel<4, W, 1, false, A>), grid, dim3(kThreads), 0,                 \
+  hipLaunchKernelGGL((gemm_kernel<4, W, 1, false, true, A>), grid, dim3(kThreads), 0,                 \
                      (hipStream_t)stream, qw, qsz, (const _Float16*)x, nullptr, (_Float16*)y, M, \
                      N, K, 128, group_magic(128), tiles_m, tiles_n)
   const int a = abl & 3;
