@@ -84,8 +84,7 @@ __device__ __forceinline__ Piece<BITS> load_piece(const uint32_t* __restrict__ p
 }
 
 // the same with the non-temporal hint on the streamed (read-once) weight bytes: measured
-// -5 % per 4096 x 4096 GEMV launch (tools/dev/gemv_lab.hip); int3's 12-byte piece keeps the plain
-// load (no 3-dword vector type without 16-byte padding)
+// -5 % per 4096 x 4096 GEMV launch (tools/dev/gemv_lab.hip)
 template <int BITS>
 __device__ __forceinline__ Piece<BITS> load_piece_nt(const uint32_t* __restrict__ p) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -102,8 +101,10 @@ __device__ __forceinline__ Piece<BITS> load_piece_nt(const uint32_t* __restrict_
   } else if constexpr (BITS == 2) {
     const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
     c.w[0] = v.x; c.w[1] = v.y;
-  } else {
-    c = load_piece<BITS>(p);
+  } else {  // 12 B: a 3-dword vector load (global_load_dwordx3 nt; only 4-byte alignment needed)
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+    const u32x3 v = __builtin_nontemporal_load(reinterpret_cast<const u32x3*>(p));
+    c.w[0] = v.x; c.w[1] = v.y; c.w[2] = v.z;
   }
   return c;
 }
