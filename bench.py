@@ -50,6 +50,20 @@ def algo_bytes(M, N, K, bits, group, zero_bytes=1):
     return 2 * M * K + N * K * bits // 8 + N * (K // group) * (2 + zero_bytes) + 2 * M * N
 
 
+def _pmc_traffic(workload):
+    """HBM bytes per launch from the newest committed PMC pass for this workload
+    (profiles/*_<workload>_pmc.json, written by tools/pmc_traffic.py from rocprofv3 --pmc
+    FETCH_SIZE with the gfx950 x2 correction), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_pmc.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    d["file"] = os.path.relpath(files[-1], ROOT)
+    return d
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,6 +226,10 @@ def main():
                 "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
     roof["traffic"] = None
+    pmc = _pmc_traffic(args.workload)
+    if pmc is not None:
+        roof["traffic"] = round(pmc["fetch_bytes_per_launch"])
+        roof["traffic_source"] = pmc["file"]
     roof["bytes_per_launch"] = nbytes
     roof["bytes_read_per_launch"] = read_bytes
     roof["us_per_launch"] = round(per_launch_s * 1e6, 3)
