@@ -18,7 +18,7 @@ from typing import Optional, Tuple
 import torch
 from torch import nn
 
-from quant.int_linear import QuantLinear
+from quant.int_linear import FusedPackedLinear, QuantLinear
 from quant.int_matmul import QuantMatMul
 from quant.omni_norm import OmniLlamaRMSNorm
 
@@ -95,8 +95,17 @@ class QuantLlamaMLP(nn.Module):
         self.down_proj = QuantLinear(org_module.down_proj, args.weight_quant_params, args.act_quant_params)
         self.up_proj = QuantLinear(org_module.up_proj, args.weight_quant_params, args.act_quant_params)
         self.act_fn = _act(hidden_act)
+        self.gate_up = None  # FusedPackedLinear after fuse_packed()
+
+    def fuse_packed(self):
+        """gate_proj + up_proj as one fused packed launch (both read x)."""
+        self.gate_up = FusedPackedLinear([self.gate_proj, self.up_proj])
+        return self
 
     def forward(self, x):
+        if self.gate_up is not None and not self.gate_proj.use_act_quant:
+            gate, up = self.gate_up(x)
+            return self.down_proj(self.act_fn(gate) * up)
         return self.down_proj(self.act_fn(self.gate_proj(x)) * self.up_proj(x))
 
 
@@ -131,6 +140,17 @@ class QuantLlamaAttention(nn.Module):
         self.pv_matmul = QuantMatMul(args.p_quant_params, args.v_quant_params, matmul_func=torch.matmul)
         self.use_weight_quant = False
         self.use_act_quant = False
+        self.qkv = None  # FusedPackedLinear after fuse_packed()
+
+    def fuse_packed(self):
+        """q_proj + k_proj + v_proj as one fused packed launch (all read the normed hidden)."""
+        self.qkv = FusedPackedLinear([self.q_proj, self.k_proj, self.v_proj])
+        return self
+
+    def _project(self, hidden_states):
+        if self.qkv is not None and not self.q_proj.use_act_quant:
+            return self.qkv(hidden_states)
+        return self.q_proj(hidden_states), self.k_proj(hidden_states), self.v_proj(hidden_states)
 
     def _shape(self, tensor: torch.Tensor, seq_len: int, bsz: int):
         return tensor.view(bsz, seq_len, self.num_heads, self.head_dim).transpose(1, 2).contiguous()
@@ -146,9 +166,10 @@ class QuantLlamaAttention(nn.Module):
     ):
         bsz, q_len, _ = hidden_states.size()
         act_dtype = hidden_states.dtype
-        query_states = self.q_proj(hidden_states).view(bsz, q_len, self.num_heads, self.head_dim).transpose(1, 2).type(torch.float32)
-        key_states = self.k_proj(hidden_states).view(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
-        value_states = self.v_proj(hidden_states).view(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
+        q, k, v = self._project(hidden_states)
+        query_states = q.reshape(bsz, q_len, self.num_heads, self.head_dim).transpose(1, 2).type(torch.float32)
+        key_states = k.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
+        value_states = v.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
 
         kv_seq_len = key_states.shape[-2]
         if past_key_value is not None:
@@ -179,7 +200,9 @@ class QuantLlamaAttention(nn.Module):
                 raise ValueError(
                     f"Attention mask should be of size {(bsz, 1, q_len, kv_seq_len)}, but is {attention_mask.size()}")
             attn_weights = attn_weights + attention_mask
-            attn_weights = torch.max(attn_weights, torch.tensor(torch.finfo(attn_weights.dtype).min, device=attn_weights.device))
+            # == torch.max(w, torch.tensor(finfo.min)) of the reference (:155-157), without the
+            # host->device scalar copy (keeps the layer capturable in a HIP graph)
+            attn_weights = attn_weights.clamp_min(torch.finfo(attn_weights.dtype).min)
 
         attn_weights = nn.functional.softmax(attn_weights, dim=-1, dtype=torch.float32).to(query_states.dtype)
         attn_weights = self.pv_matmul.quant_x1(attn_weights)
@@ -248,6 +271,12 @@ class QuantLlamaDecoderLayer(nn.Module):
         for name, m in self.named_modules():
             if isinstance(m, (QuantLinear, QuantMatMul)):
                 m.set_quant_state(weight_quant, act_quant)
+
+    def fuse_packed_projections(self):
+        """After packing: q/k/v and gate/up each become one fused launch."""
+        self.self_attn.fuse_packed()
+        self.mlp.fuse_packed()
+        return self
 
     @torch.no_grad()
     def smooth_and_quant_inplace(self):

@@ -79,7 +79,7 @@ class QuantOPTAttention(nn.Module):
                 raise ValueError(
                     f"Attention mask should be of size {(bsz, 1, tgt_len, src_len)}, but is {attention_mask.size()}")
             attn_weights = attn_weights.view(bsz, self.num_heads, tgt_len, src_len) + attention_mask
-            attn_weights = torch.max(attn_weights, torch.tensor(torch.finfo(attn_weights.dtype).min, device=attn_weights.device))
+            attn_weights = attn_weights.clamp_min(torch.finfo(attn_weights.dtype).min)  # == torch.max(w, tensor(min))
             attn_weights = attn_weights.view(bsz * self.num_heads, tgt_len, src_len)
         if attn_weights.dtype == torch.float16:
             attn_weights = nn.functional.softmax(attn_weights, dim=-1, dtype=torch.float32).to(torch.float16)

@@ -161,3 +161,48 @@ class QuantLinear(nn.Module):
         if self.packed:
             s += f", packed=int{self.wbits} g{self.group}"
         return s
+
+
+class FusedPackedLinear(nn.Module):
+    """Several packed QuantLinear that read the same input (q/k/v, gate/up) as ONE fused
+    dequant-GEMV/GEMM launch over their concatenated rows.
+
+    The tiled layout concatenates along output rows tile by tile (each member's out_features must
+    be a multiple of 16), so every output element is computed by exactly the kernel code path it
+    takes unfused — results are bit-identical, with one launch instead of len(members)."""
+
+    def __init__(self, members):
+        super().__init__()
+        if not members or not all(m.packed for m in members):
+            raise ValueError("FusedPackedLinear needs packed QuantLinear members")
+        m0 = members[0]
+        for m in members:
+            if (m.in_features, m.wbits, m.group) != (m0.in_features, m0.wbits, m0.group):
+                raise ValueError("fused members must share in_features, bits and group")
+            if m.out_features % qlin.TILE_N:
+                raise ValueError("fused members need out_features % 16 == 0")
+        self.splits = [m.out_features for m in members]
+        self.in_features = m0.in_features
+        self.out_features = sum(self.splits)
+        self.wbits, self.group = m0.wbits, m0.group
+        self.register_buffer("qweight", torch.cat([m.qweight for m in members], dim=0))
+        self.register_buffer("qsz", torch.cat([m.qsz for m in members], dim=0))
+        self.qflags = 0
+        for m in members:
+            self.qflags |= m.qflags
+        biases = [m.bias for m in members]
+        if any(b is not None for b in biases):
+            dev, dt = self.qweight.device, torch.float16
+            self.register_buffer("bias", torch.cat(
+                [b.to(dt) if b is not None else torch.zeros(n, dtype=dt, device=dev)
+                 for b, n in zip(biases, self.splits)]))
+        else:
+            self.bias = None
+
+    def forward(self, x):
+        xin = x if x.dtype == torch.float16 else x.to(torch.float16)
+        y = qlin.linear(xin.contiguous(), self.qweight, self.qsz, self.bias, self.out_features,
+                        self.in_features, self.wbits, self.group, self.qflags)
+        if x.dtype != torch.float16:
+            y = y.to(x.dtype)
+        return torch.split(y, self.splits, dim=-1)

@@ -61,3 +61,22 @@ def test_packed_ppl_matches_fake_quant():
         pack_quant_linears(layer)
     ppl_pk = eval_ppl(model, testenc, seqlen=128)
     assert np.isfinite(ppl_fq) and abs(ppl_pk - ppl_fq) / ppl_fq < 1e-3, (ppl_fq, ppl_pk)
+
+
+def test_fused_projections_bit_identical():
+    """q/k/v and gate/up fused into one packed launch each (FusedPackedLinear): every output
+    element takes the same kernel path as unfused, so logits must be bit-identical."""
+    cfg = _cfg(layers=2)
+    model = build_random_quant_llama(cfg, quant_args(4, 128), seed=13, device="cuda",
+                                     dtype=torch.float16)
+    rtn_quantize_(model, pack=True)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    toks = [torch.randint(0, cfg.vocab_size, (1, T), device="cuda", generator=g)
+            for T in (1, 5, 70)]
+    with torch.no_grad():
+        ref = [model(x) for x in toks]
+        for layer in model.layers:
+            layer.fuse_packed_projections()
+        got = [model(x) for x in toks]
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
