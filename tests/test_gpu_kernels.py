@@ -193,3 +193,28 @@ def test_invalid_arguments_raise():
                              17, N, K, 4, group, None) == 1
     assert lib.qlin_gemm_f16(None, qsz.data_ptr(), 0, x.data_ptr(), None, y.data_ptr(),
                              1, N, K, 4, group, None, None) == 1
+
+
+@pytest.mark.parametrize("bits,group", [(4, 128), (3, 64), (2, 64), (8, 128)])
+def test_gptq_checkpoint_conversion(bits, group):
+    """AutoGPTQ tensors (restated format, oracle/gptq_format.py) -> tiled layout: the packed
+    layer's W_dq equals AutoGPTQ's fp16 dequant bit for bit, and its forward matches x @ W^T."""
+    from oracle import gptq_format as OG
+    from quant import gptq
+    rs = np.random.RandomState(bits + group)
+    K, N = 1024, 384
+    G = K // group
+    q = rs.randint(0, 2 ** bits, size=(K, N))
+    z = rs.randint(1, 2 ** bits, size=(G, N))
+    s = (rs.rand(G, N) * 0.01 + 1e-3).astype(np.float16)
+    tensors = {"lin.qweight": torch.from_numpy(OG.pack_qweight(q, bits).view(np.int32)),
+               "lin.qzeros": torch.from_numpy(OG.pack_qzeros(z, bits).view(np.int32)),
+               "lin.scales": torch.from_numpy(s),
+               "lin.g_idx": torch.from_numpy((np.arange(K) // group).astype(np.int32)),
+               "lin.bias": torch.from_numpy((rs.randn(N) * 0.1).astype(np.float16))}
+    ql = gptq.packed_quant_linear(tensors, "lin", bits)
+    ref_w = OG.dequant(q, z, s, np.arange(K) // group)
+    assert bit_equal(n(ql.dequantized_weight()), ref_w)
+    x = rand_x(3, K, seed=2)
+    y = ql(t(x).unsqueeze(0))[0]
+    assert_close_to_ref(n(y), O.linear_ref(x, ref_w, tensors["lin.bias"].numpy()))

@@ -29,3 +29,31 @@ extern "C" int dev_empty(int blocks, void* out, void* st) {
   hipLaunchKernelGGL(empty_k, dim3(blocks), dim3(256), 0, (hipStream_t)st, (uint32_t*)out);
   return (int)hipGetLastError();
 }
+
+extern "C" int dev_empty_cfg(int blocks, int threads, void* out, void* st) {
+  hipLaunchKernelGGL(empty_k, dim3(blocks), dim3(threads), 0, (hipStream_t)st, (uint32_t*)out);
+  return (int)hipGetLastError();
+}
+
+// streaming read with an arbitrary grid: each thread reads `per` 16-B chunks strided by the grid
+__global__ __launch_bounds__(1024) void stream_read_g(const uint4* __restrict__ p, int64_t n16,
+                                                     uint32_t* out, int per) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  uint4 v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (j < per) v[j] = p[min(i + j * nthr, n16 - 1)];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (j < per) acc ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+  if (acc == 0x12345678u) out[0] = acc;
+}
+extern "C" int dev_stream_cfg(const void* p, int64_t bytes, int blocks, int threads, void* out, void* st) {
+  const int64_t n16 = bytes / 16;
+  const int per = (int)((n16 + (int64_t)blocks * threads - 1) / ((int64_t)blocks * threads));
+  if (per > 8) return 1;
+  hipLaunchKernelGGL(stream_read_g, dim3(blocks), dim3(threads), 0, (hipStream_t)st, (const uint4*)p, n16, (uint32_t*)out, per);
+  return (int)hipGetLastError();
+}
