@@ -207,6 +207,20 @@ __device__ __forceinline__ GroupQ make_group(_Float16 s, int zp) {
   return g;
 }
 
+// the same straight from a qsz word, in fp16 arithmetic: int16 -> fp16 is exact for |zp| <= 2048
+// and off + zp is exact for |zp| <= 1024 (narrow), so no int -> fp32 -> fp16 round trip
+template <int BITS, bool WIDE>
+__device__ __forceinline__ GroupQ make_group_w(uint32_t w) {
+  if constexpr (WIDE) return make_group<BITS, true>(sz_scale(w), sz_zero(w));
+  GroupQ g;
+  const _Float16 s = sz_scale(w);
+  const _Float16 z = (_Float16)(int16_t)(w >> 16);
+  g.ss = h2{s, s};
+#pragma unroll
+  for (int P = 0; P < 4; ++P) g.zz[P] = h2{z, z} + h2{(_Float16)pair_off<BITS>(P), (_Float16)pair_off<BITS>(P)};
+  return g;
+}
+
 // exact dequantized fp16 values of k-step S: out[P] = (w_2P, w_2P+1) = RN16(RN16(u - zp) * s)
 template <int BITS, bool WIDE, int S>
 __device__ __forceinline__ void dequant_step(const Piece<BITS>& c, const Magics& mg, const GroupQ& g,

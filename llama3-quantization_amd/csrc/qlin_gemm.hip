@@ -165,7 +165,7 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const uint32_t sw = ss[((wn * NB + nb) * GPT + slot) * 16 + n_in];
-      gq[nb] = make_group<BITS, WIDE>(sz_scale(sw), sz_zero(sw));
+      gq[nb] = make_group_w<BITS, WIDE>(sw);
     }
   };
 

@@ -127,7 +127,7 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
     const int k0 = kt * kTileK + 32 * S;
     if (FULL || k0 < g.K) {  // wave-uniform
       uint32_t v[4];
-      const GroupQ gq = make_group<BITS, WIDE>(sz_scale(t.sz[slot]), sz_zero(t.sz[slot]));
+      const GroupQ gq = make_group_w<BITS, WIDE>(t.sz[slot]);
       dequant_step<BITS, WIDE, S>(t.pc, mg, gq, v);
       const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, acc, 0, 0, 0);
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void dequant_kernel(
     const int k0 = kt * kTileK + 32 * S + 8 * q;
     if (k0 >= K) return;
     const uint32_t sw = qsz[sz_index(nt, k0 / group, G, n_in)];
-    const GroupQ g = make_group<BITS, WIDE>(sz_scale(sw), sz_zero(sw));
+    const GroupQ g = make_group_w<BITS, WIDE>(sw);
     uint32_t o[4];
     dequant_step<BITS, WIDE, S>(c, mg, g, o);
     *reinterpret_cast<uint4*>(w + row * K + k0) = make_uint4(o[0], o[1], o[2], o[3]);
