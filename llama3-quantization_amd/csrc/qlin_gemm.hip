@@ -35,15 +35,15 @@ constexpr int64_t kSkinnyMaxM = 64;   // qlin_linear_f16: M <= this runs the GEM
 typedef __attribute__((address_space(3))) void* lds_ptr;
 typedef __attribute__((address_space(1))) void* gbl_ptr;
 
-// Wave tiles are 128 (or 64) rows x 128 columns: 8 B fragments dequantized per k-step feed
-// MB x 8 MFMAs, so the 13 VALU per fragment fit the issue slots the MFMAs leave free.
-// WIDE_N: block 128 x 512, 4 waves side by side in N (each B element dequantized once; 1.3x the
-// MFMA rate of the narrow tile at M >= 8192) — int2/3/4 when the grid has >= 2 blocks per CU;
-// otherwise block 128 x 256, waves 2 x 2 (twice the blocks; int8 always: twice the code bytes).
+// Wave tiles are 128 rows x 128 (wide) or 64 (narrow) columns: each B fragment dequantized per
+// k-step feeds 8 MFMAs (one per 16-row block), so its 13 VALU fit the issue slots the MFMAs leave
+// free, and the 4 waves sit side by side in N, so every B element is dequantized once per block.
+// WIDE_N: block 128 x 512 (int2/3/4 when the grid has >= 2 blocks per CU); otherwise 128 x 256
+// (twice the blocks; int8 always: twice the code bytes).
 template <int BITS, bool WIDE_N> struct Cfg {
   static constexpr int BN = WIDE_N ? 512 : 256;
-  static constexpr int WGN = BN / 128, WGM = 4 / WGN;  // waves along N, along M
-  static constexpr int WM = BM / WGM, WN = 128;
+  static constexpr int WGN = 4, WGM = 1;  // the 4 waves side by side in N: B dequantized once
+  static constexpr int WM = BM / WGM, WN = BN / WGN;
   static constexpr int MB = WM / 16, NB = WN / kTileN;  // 16 x 16 MFMA blocks per wave
   static constexpr int RT = BN / kTileN;                // packed row tiles per block
   static constexpr int A_BYTES = BM * BK * 2;           // 32 KB
