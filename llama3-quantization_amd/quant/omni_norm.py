@@ -48,6 +48,12 @@ class OmniLlamaRMSNorm(nn.Module):
             weight, bias = self.temp_weight, self.temp_bias
         else:
             weight, bias = self.weight, self.bias
+        # weight (fp16) * hidden (fp32) promotes to fp32: multiplying by the fp32 copy of the
+        # weight is the same arithmetic (fp16 -> fp32 is exact) and takes PyTorch's vectorised
+        # same-dtype kernel instead of the mixed-dtype one (measured 41 us vs ~3 us per call on
+        # MI355X for a 4096-wide decode token)
+        if weight.dtype != hidden_states.dtype:
+            weight = weight.to(hidden_states.dtype)
         if bias is not None:
             return (weight * hidden_states + bias).to(input_dtype)
         return (weight * hidden_states).to(input_dtype)
