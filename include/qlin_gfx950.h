@@ -127,6 +127,19 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
                     const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
                     int group, void* stream);
 
+/*
+ * Fused decode attention (one query token per sequence), for the quantized LLaMA layer's
+ * attention core (models/int_llama_layer.py:137-165 of the reference: repeat_kv, fp32 QK^T bmm,
+ * / sqrt(head_dim), + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV bmm) on an fp16 K/V
+ * cache; fp32 arithmetic, equal to the reference up to fp32 summation order.
+ *   q    fp32 [B, Hq, D] (after RoPE);  k, v  fp16 [B, Hkv, L, D];  mask  fp16 [B, L] additive or
+ *   NULL;  out  fp32 [B, Hq, D];  scale_div = sqrt(D) (the reference divides the scores by it).
+ *   D == 128, Hq / Hkv in {1, 2, 4, 8}, L <= 4096.
+ */
+int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
+                     float* out, int64_t B, int Hq, int Hkv, int64_t L, int D, float scale_div,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

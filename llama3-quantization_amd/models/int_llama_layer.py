@@ -18,6 +18,7 @@ from typing import Optional, Tuple
 import torch
 from torch import nn
 
+from quant import qlin
 from quant.int_linear import FusedPackedLinear, QuantLinear
 from quant.int_matmul import QuantMatMul
 from quant.omni_norm import OmniLlamaRMSNorm
@@ -141,11 +142,21 @@ class QuantLlamaAttention(nn.Module):
         self.use_weight_quant = False
         self.use_act_quant = False
         self.qkv = None  # FusedPackedLinear after fuse_packed()
+        self.decode_kernel = False  # qlin_attn_decode for one-token steps (fuse_packed turns it on)
 
     def fuse_packed(self):
-        """q_proj + k_proj + v_proj as one fused packed launch (all read the normed hidden)."""
+        """q_proj + k_proj + v_proj as one fused packed launch (all read the normed hidden), and
+        the fused decode-attention kernel for one-token steps."""
         self.qkv = FusedPackedLinear([self.q_proj, self.k_proj, self.v_proj])
+        self.decode_kernel = True
         return self
+
+    def _attn_bypassed(self):
+        """QuantMatMul quantizers are identity (abits >= 16 or act quant off)."""
+        for mm in (self.qkt_matmul, self.pv_matmul):
+            if mm.use_act_quant and (mm.x1_quantizer.n_bits < 16 or mm.x2_quantizer.n_bits < 16):
+                return False
+        return True
 
     def _project(self, hidden_states):
         if self.qkv is not None and not self.q_proj.use_act_quant:
@@ -183,6 +194,15 @@ class QuantLlamaAttention(nn.Module):
             key_states = torch.cat([past_key_value[0], key_states], dim=2)
             value_states = torch.cat([past_key_value[1], value_states], dim=2)
         past_key_value = (key_states, value_states) if use_cache else None
+
+        if (self.decode_kernel and q_len == 1 and not output_attentions and self._attn_bypassed()
+                and qlin.attn_decode_supported(query_states, key_states, attention_mask)):
+            # fused decode attention: same fp32 arithmetic as the path below (repeat_kv, QK^T,
+            # / sqrt(d), + mask, clamp, softmax, PV) up to summation order
+            attn_output = qlin.attn_decode(query_states, key_states, value_states, attention_mask,
+                                           math.sqrt(self.head_dim))
+            attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
+            return self.o_proj(attn_output), None, past_key_value
 
         key_states = repeat_kv(key_states, self.num_key_value_groups)
         value_states = repeat_kv(value_states, self.num_key_value_groups)

@@ -44,6 +44,7 @@ SIGNATURES = {
     "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
+    "qlin_attn_decode": ([_p, _p, _p, _p, _p, _l, _i, _i, _l, _i, ctypes.c_float, _p], _i),
 }
 
 
@@ -262,3 +263,37 @@ def gemv(x, qweight, qsz, bias, N, K, bits, group, flags=0):
 def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0):
     return _linear_call("qlin_gemm_f16", x, qweight, qsz, bias, N, K, bits, group, flags,
                         extra=(None,))
+
+
+ATTN_MAX_L = 4096
+ATTN_D = 128
+
+
+def attn_decode_supported(q, k, mask=None):
+    """Whether qlin_attn_decode takes this call (see attn_decode)."""
+    return (q.is_cuda and q.dim() == 4 and q.shape[2] == 1 and q.shape[-1] == ATTN_D
+            and q.dtype == torch.float32 and k.dtype == torch.float16
+            and k.shape[2] <= ATTN_MAX_L and q.shape[1] % k.shape[1] == 0
+            and q.shape[1] // k.shape[1] in (1, 2, 4, 8)
+            and (mask is None or (mask.dtype == torch.float16 and mask.shape[-2] == 1)))
+
+
+def attn_decode(q, k, v, mask, scale_div):
+    """softmax(q k^T / scale_div + mask) v for one query token: q fp32 [B, Hq, 1, D], k/v fp16
+    [B, Hkv, L, D], mask fp16 [B, 1, 1, L] or None -> fp32 [B, Hq, 1, D]."""
+    _dev(q, k, v)
+    if not attn_decode_supported(q, k, mask):
+        raise ValueError("attn_decode: unsupported shapes / dtypes")
+    B, Hq, _, D = q.shape
+    Hkv, L = k.shape[1], k.shape[2]
+    k = k.contiguous()
+    v = v.contiguous()
+    m = None
+    if mask is not None:
+        m = mask.reshape(B, L).contiguous() if mask.shape[0] == B else \
+            mask.expand(B, 1, 1, L).reshape(B, L).contiguous()
+    out = torch.empty(B, Hq, 1, D, dtype=torch.float32, device=q.device)
+    rc = load_library().qlin_attn_decode(_ptr(q.contiguous()), _ptr(k), _ptr(v), _ptr(m), _ptr(out),
+                                         B, Hq, Hkv, L, D, float(scale_div), _stream(q))
+    _check(rc, "qlin_attn_decode")
+    return out

@@ -93,7 +93,10 @@ def main():
            "fused_weight_GBps": round(wbytes / res["packed_fused_us"] / 1e3, 1),
            "rel_err_packed_vs_fake_quant": float((y_pk.float() - y_fq.float()).abs().max()
                                                  / y_fq.float().abs().max()),
-           "fused_equals_unfused": bool(torch.equal(y_pk, y_fu)),
+           # fused = fused projections (bit-identical) + fused decode attention (fp32 summation
+           # order differs from the bmm), so the comparison is a relative error, not equality
+           "rel_err_fused_vs_unfused": float((y_fu.float() - y_pk.float()).abs().max()
+                                             / y_pk.float().abs().max()),
            "est_32_layer_token_ms": round(res["packed_fused_us"] * 32 / 1e3, 3)}
     print(json.dumps(out))
 
