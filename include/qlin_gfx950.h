@@ -135,10 +135,16 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
  *   q    fp32 [B, Hq, D] (after RoPE);  k, v  fp16 [B, Hkv, L, D];  mask  fp16 [B, L] additive or
  *   NULL;  out  fp32 [B, Hq, D];  scale_div = sqrt(D) (the reference divides the scores by it).
  *   D == 128, Hq / Hkv in {1, 2, 4, 8}, L <= 4096.
+ * The cache is split over blocks along L.  qlin_attn_decode_partials_bytes() returns the bytes
+ * of `partials` scratch a call needs (0: none, pass NULL; -1: unsupported shapes); `counters` is
+ * int32 [>= B * Hkv], zero-filled before its first use and left zero-filled by every call (the
+ * merging block resets it), so one counter buffer serves all later calls on the same stream,
+ * graph replays included; do not share it between streams running concurrently.
  */
+int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L);
 int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
                      float* out, int64_t B, int Hq, int Hkv, int64_t L, int D, float scale_div,
-                     void* stream);
+                     float* partials, int32_t* counters, void* stream);
 
 #ifdef __cplusplus
 }

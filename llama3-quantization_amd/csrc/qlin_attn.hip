@@ -5,141 +5,352 @@
 // QK^T bmm, the division by sqrt(head_dim), the additive mask with the finfo.min clamp, the fp32
 // softmax and the fp32 PV bmm — six PyTorch kernels plus two K/V expansions and two fp16 -> fp32
 // copies of the whole cache per layer and token — with one kernel that reads each K/V row once
-// for all the query heads of its group (GQA) and keeps scores in LDS.
+// for all the query heads of its group (GQA).
 //
-// Arithmetic: fp32 throughout, as the reference (q is fp32, K/V are upcast exactly); the dot
-// products and sums run in a different order than hipBLASLt's bmm, so results agree to fp32
-// rounding, not bit for bit.
+// Split-L ("flash-decoding"): the grid is (B * Hkv) x S blocks, each over a chunk of `chunk`
+// cache positions (a multiple of 64, chosen on the host for ~kTargetBlocks blocks: one sequence
+// at batch 1 has only Hkv = 8 KV heads, far too few blocks to pull the cache at HBM rate).  A
+// block writes its chunk's (max, sum, unnormalised P V) to `partials`; the last block of a
+// (b, kv head) to count in merges the S partials and resets the counter, so the kernel is
+// graph-replayable with no memset.
+//
+// Latency: decode attention at batch 1 is a chain of dependent memory round trips, not a bandwidth
+// problem, so a block issues the K rows, V rows and mask of its first 64 positions before it waits
+// on q, and the merge reads the partials with all 256 threads (one coalesced 256-B row per wave
+// and load).
+//
+// Cross-block hand-off: the partials are written and read with agent-scope (sc1) accesses and the
+// writer drains its stores (vmcnt) before the block barrier and the counter atomic.  A device-scope
+// __threadfence() would do the same with an L2 writeback + invalidate per wave (buffer_wbl2 /
+// buffer_inv), which costs 2-5x the kernel at batch 1 on the 8-XCD part (tools/dev/attn_ab.py).
+//
+// Arithmetic: fp32 throughout, as the reference (q is fp32, K/V are upcast exactly); dot products
+// and sums run in a different order than hipBLASLt's bmm and the softmax is merged across chunks
+// (exp(m_c - M) rescaling), so results agree with the reference to fp32 rounding, not bit for bit.
 #include "qlin_common.h"  // QLIN_OK / QLIN_EINVAL
 #include "../../include/qlin_gfx950.h"
 
 namespace {
 
-constexpr int kD = 128;             // head_dim
-constexpr int kThreads = 256;
-constexpr int kMaxGroup = 8;        // query heads per KV head
-constexpr int kMaxL = 4096;         // scores live in LDS: kMaxGroup * kMaxL fp32 = 128 KB
-static_assert(kMaxGroup * kMaxL * 4 <= 128 * 1024, "scores must fit the LDS budget");
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float block_max(float v, float* red) {
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  __syncthreads();
-  if (l == 0) red[w] = v;
-  __syncthreads();
-  float r = red[0];
-  for (int i = 1; i < kThreads / 64; ++i) r = fmaxf(r, red[i]);
-  return r;
+constexpr int kD = 128;          // head_dim
+constexpr int kThreads = 256;    // 4 waves
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxGroup = 8;     // query heads per KV head
+constexpr int kMaxL = 4096;
+constexpr int kSub = 64;         // positions per pass (8 lanes x 16 dims per K row)
+constexpr int kMaxChunk = 512;   // scores of one chunk live in LDS: 512 x 8 fp32 = 16 KB
+constexpr int kMaxSplit = kMaxL / kSub;
+constexpr int kTargetBlocks = 1024;
+
+struct Split {
+  int chunk, S;
+};
+
+Split choose_split(int64_t B, int Hkv, int64_t L) {
+  const int64_t heads = B * Hkv;
+  int64_t want = (kTargetBlocks + heads - 1) / heads;  // splits per (b, kv head)
+  if (want < 1) want = 1;
+  int64_t chunk = (L + want - 1) / want;
+  chunk = (chunk + kSub - 1) / kSub * kSub;
+  if (chunk > kMaxChunk) chunk = kMaxChunk;
+  return Split{(int)chunk, (int)((L + chunk - 1) / chunk)};
 }
 
-__device__ __forceinline__ float block_sum(float v, float* red) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  __syncthreads();
-  if (l == 0) red[w] = v;
-  __syncthreads();
-  float r = 0.f;
-  for (int i = 0; i < kThreads / 64; ++i) r += red[i];
-  return r;
+// Dev ablation hook (tools/dev/Makefile libattn<N>.so): 0 = product (sc1 hand-off, see above),
+// 1 = device-scope __threadfence() in every thread instead.
+#ifndef ATTN_FENCE_MODE
+#define ATTN_FENCE_MODE 0
+#endif
+
+__device__ __forceinline__ void part_store(float* p, float v) {
+#if ATTN_FENCE_MODE == 0
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
 }
 
-// one block per (batch, KV head); GRP query heads share the K/V rows
+__device__ __forceinline__ float part_load(const float* p) {
+#if ATTN_FENCE_MODE == 0
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  return *p;
+#endif
+}
+
+__device__ __forceinline__ float h2f(uint32_t w, int hi) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? (w >> 16) : (w & 0xFFFFu)));
+}
+
+// partials: [o fp32 B*Hkv*S*GRP*D][m, l fp32 B*Hkv*S*GRP*2]; counters: int32 [B*Hkv], zero
+
 template <int GRP>
 __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
     const float* __restrict__ q, const _Float16* __restrict__ k, const _Float16* __restrict__ v,
-    const _Float16* __restrict__ mask, float* __restrict__ out, int Hq, int Hkv, int L,
-    float scale_div) {
+    const _Float16* __restrict__ mask, float* __restrict__ out, int Hq, int Hkv, int L, int chunk,
+    int S, float scale_div, int* __restrict__ counters, float* __restrict__ part_o,
+    float* __restrict__ part_ml) {
   __shared__ float qs[GRP][kD];
-  __shared__ float sc[GRP][kMaxL];
-  __shared__ float red[kThreads / 64];
-  const int b = blockIdx.x / Hkv, hk = blockIdx.x % Hkv;
-  const int tid = threadIdx.x;
+  __shared__ float sc[kMaxChunk][GRP];     // scores, then probabilities (position-major)
+  __shared__ float po[kWaves][GRP * kD];   // per-wave P V (and merge) partial sums
+  __shared__ float cm[GRP], cl[GRP];       // chunk max / sum; merged denominators
+  __shared__ float mw[kMaxSplit][GRP];     // merge: chunk maxima, then weights
+  __shared__ float ml_l[kMaxSplit][GRP];   // merge: chunk sums
+  __shared__ int last;
+
+  const int bh = blockIdx.x;  // b * Hkv + kv head
+  const int split = blockIdx.y;
+  const int b = bh / Hkv, hk = bh % Hkv;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int sub = tid & 7, tl = tid >> 3;  // score passes: 8 lanes x 16 dims per K row
+  const int t0 = split * chunk;
+  const int n = min(chunk, L - t0);  // positions in this chunk (>= 1)
+
+  const _Float16* kb = k + ((int64_t)bh * L + t0) * kD;
+  const uint32_t* vb = reinterpret_cast<const uint32_t*>(v + ((int64_t)bh * L + t0) * kD) + lane;
+  const _Float16* mb = mask ? mask + (int64_t)b * L + t0 : nullptr;
+
+  // issue the first pass's K rows, V words and mask before anything waits
+  u32x4 kw[2][2];
+  float mv[2];
+  auto load_k = [&](int tb) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = min(tb + 32 * u + tl, n - 1);
+      const u32x4* kr = reinterpret_cast<const u32x4*>(kb + (int64_t)t * kD + 16 * sub);
+      kw[u][0] = __builtin_nontemporal_load(kr);
+      kw[u][1] = __builtin_nontemporal_load(kr + 1);
+      mv[u] = mb ? (float)mb[t] : 0.f;
+    }
+  };
+  uint32_t vw[kSub / kWaves];  // PV: lane = dim pair, wave = every 4th position
+  auto load_v = [&](int tb) {
+#pragma unroll
+    for (int u = 0; u < kSub / kWaves; ++u) {
+      const int t = min(tb + wave + kWaves * u, n - 1);
+      vw[u] = __builtin_nontemporal_load(vb + (int64_t)t * (kD / 2));
+    }
+  };
+  load_k(0);
+  load_v(0);
+
   const float* qb = q + ((int64_t)b * Hq + (int64_t)hk * GRP) * kD;
   for (int i = tid; i < GRP * kD; i += kThreads) qs[i / kD][i % kD] = qb[i];
   __syncthreads();
-  const _Float16* kb = k + ((int64_t)b * Hkv + hk) * (int64_t)L * kD;
-  const _Float16* vb = v + ((int64_t)b * Hkv + hk) * (int64_t)L * kD;
-  const _Float16* mb = mask ? mask + (int64_t)b * L : nullptr;
 
-  // scores: one K row per thread (16 x 16-byte loads), GRP dot products
-  for (int t = tid; t < L; t += kThreads) {
-    float acc[GRP];
+  // scores (the next pass's K rows are in flight while this pass computes)
+  for (int tb = 0; tb < n; tb += kSub) {
+    u32x4 kc[2][2];
+    float mc[2];
 #pragma unroll
-    for (int g = 0; g < GRP; ++g) acc[g] = 0.f;
-    const uint4* kr = reinterpret_cast<const uint4*>(kb + (int64_t)t * kD);
-#pragma unroll 4
-    for (int c = 0; c < kD / 8; ++c) {
-      const uint4 w = kr[c];
-      const _Float16* hv = reinterpret_cast<const _Float16*>(&w);
+    for (int u = 0; u < 2; ++u) {
+      kc[u][0] = kw[u][0];
+      kc[u][1] = kw[u][1];
+      mc[u] = mv[u];
+    }
+    if (tb + kSub < n) load_k(tb + kSub);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float kf = (float)hv[j];
+    for (int u = 0; u < 2; ++u) {
+      const int t = tb + 32 * u + tl;
+      float acc[GRP];
 #pragma unroll
-        for (int g = 0; g < GRP; ++g) acc[g] = fmaf(qs[g][8 * c + j], kf, acc[g]);
+      for (int g = 0; g < GRP; ++g) acc[g] = 0.f;
+      const _Float16* hv = reinterpret_cast<const _Float16*>(kc[u]);
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+#pragma unroll
+        for (int g = 0; g < GRP; ++g) {
+          const float4 qq = *reinterpret_cast<const float4*>(&qs[g][16 * sub + j]);
+          acc[g] = fmaf(qq.x, (float)hv[j], acc[g]);
+          acc[g] = fmaf(qq.y, (float)hv[j + 1], acc[g]);
+          acc[g] = fmaf(qq.z, (float)hv[j + 2], acc[g]);
+          acc[g] = fmaf(qq.w, (float)hv[j + 3], acc[g]);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < GRP; ++g) {
+        acc[g] += __shfl_xor(acc[g], 1);
+        acc[g] += __shfl_xor(acc[g], 2);
+        acc[g] += __shfl_xor(acc[g], 4);
+      }
+      if (t < n && sub < GRP) {
+        // lane `sub` stores query head g = sub (select without dynamic register indexing)
+        float a = acc[0];
+#pragma unroll
+        for (int g = 1; g < GRP; ++g) a = (sub == g) ? acc[g] : a;
+        float s = a / scale_div + mc[u];
+        s = (s != s) ? s : fmaxf(s, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
+        sc[t][sub] = s;
       }
     }
-    const float mv = mb ? (float)mb[t] : 0.f;
-#pragma unroll
-    for (int g = 0; g < GRP; ++g) {
-      float s = acc[g] / scale_div + mv;
-      s = (s != s) ? s : fmaxf(s, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
-      sc[g][t] = s;
-    }
   }
   __syncthreads();
 
-  // softmax per query head (fp32)
-#pragma unroll 1
-  for (int g = 0; g < GRP; ++g) {
+  // chunk softmax statistics: wave w owns query heads w, w + 4 (wave-level reductions only)
+  for (int g = wave; g < GRP; g += kWaves) {
     float m = -INFINITY;
-    for (int t = tid; t < L; t += kThreads) m = fmaxf(m, sc[g][t]);
-    m = block_max(m, red);
+    for (int t = lane; t < n; t += 64) m = fmaxf(m, sc[t][g]);
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     float s = 0.f;
-    for (int t = tid; t < L; t += kThreads) {
-      const float e = expf(sc[g][t] - m);
-      sc[g][t] = e;
+    for (int t = lane; t < n; t += 64) {
+      const float e = expf(sc[t][g] - m);
+      sc[t][g] = e;
       s += e;
     }
-    s = block_sum(s, red);
-    const float inv = 1.f / s;
-    for (int t = tid; t < L; t += kThreads) sc[g][t] *= inv;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) {
+      cm[g] = m;
+      cl[g] = s;
+    }
   }
   __syncthreads();
 
-  // PV: thread (g, pair of dims) accumulates over t; V rows read once per (group, dim pair)
-  for (int o = tid; o < GRP * (kD / 2); o += kThreads) {
-    const int g = o / (kD / 2), dp = o % (kD / 2);
-    float a0 = 0.f, a1 = 0.f;
-    const uint32_t* vr = reinterpret_cast<const uint32_t*>(vb) + dp;
-    for (int t = 0; t < L; ++t) {
-      const uint32_t w = vr[(int64_t)t * (kD / 2)];
-      const float p = sc[g][t];
-      a0 = fmaf(p, (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xFFFFu)), a0);
-      a1 = fmaf(p, (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16)), a1);
+  // P V
+  {
+    float a0[GRP], a1[GRP];
+#pragma unroll
+    for (int g = 0; g < GRP; ++g) a0[g] = a1[g] = 0.f;
+    for (int tb = 0; tb < n; tb += kSub) {
+      uint32_t vc[kSub / kWaves];
+#pragma unroll
+      for (int u = 0; u < kSub / kWaves; ++u) vc[u] = vw[u];
+      if (tb + kSub < n) load_v(tb + kSub);
+#pragma unroll
+      for (int u = 0; u < kSub / kWaves; ++u) {
+        const int t = tb + wave + kWaves * u;
+        if (t < n) {
+          const float v0 = h2f(vc[u], 0), v1 = h2f(vc[u], 1);
+#pragma unroll
+          for (int g = 0; g < GRP; ++g) {
+            const float p = sc[t][g];
+            a0[g] = fmaf(p, v0, a0[g]);
+            a1[g] = fmaf(p, v1, a1[g]);
+          }
+        }
+      }
     }
-    float* ob = out + ((int64_t)b * Hq + (int64_t)hk * GRP + g) * kD + 2 * dp;
-    ob[0] = a0;
-    ob[1] = a1;
+#pragma unroll
+    for (int g = 0; g < GRP; ++g) {
+      po[wave][g * kD + 2 * lane] = a0[g];
+      po[wave][g * kD + 2 * lane + 1] = a1[g];
+    }
   }
+  __syncthreads();
+
+  const int64_t qh0 = (int64_t)b * Hq + (int64_t)hk * GRP;  // first query head of the group
+  float* ob = out + qh0 * kD;
+  if (S == 1) {
+    for (int o = tid; o < GRP * kD; o += kThreads)
+      ob[o] = (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD];
+    return;
+  }
+
+  // write this chunk's partials, then count in; the last block of (b, kv head) merges
+  float* pob = part_o + ((int64_t)bh * S + split) * GRP * kD;
+  for (int o = tid; o < GRP * kD; o += kThreads)
+    part_store(pob + o, po[0][o] + po[1][o] + po[2][o] + po[3][o]);
+  if (tid < 2 * GRP) {
+    float* ml = part_ml + ((int64_t)bh * S + split) * GRP * 2;
+    part_store(ml + tid, (tid & 1) ? cl[tid >> 1] : cm[tid >> 1]);
+  }
+#if ATTN_FENCE_MODE == 0
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sc1 stores acknowledged before the count
+#else
+  __threadfence();
+#endif
+  __syncthreads();
+  if (tid == 0)
+    last = (__hip_atomic_fetch_add(&counters[bh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            S - 1);
+  __syncthreads();
+  if (!last) return;
+#if ATTN_FENCE_MODE != 0
+  __threadfence();
+#endif
+
+  // merge: chunk statistics -> weights exp(m_s - M) and denominators sum_s w_s l_s
+  const float* mlb = part_ml + (int64_t)bh * S * GRP * 2;
+  for (int i = tid; i < S * GRP; i += kThreads) {
+    mw[i / GRP][i % GRP] = part_load(mlb + 2 * i);
+    ml_l[i / GRP][i % GRP] = part_load(mlb + 2 * i + 1);
+  }
+  __syncthreads();
+  for (int g = wave; g < GRP; g += kWaves) {
+    float M = -INFINITY;
+    for (int s = lane; s < S; s += 64) M = fmaxf(M, mw[s][g]);
+    for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
+    float den = 0.f;
+    for (int s = lane; s < S; s += 64) {
+      const float w = expf(mw[s][g] - M);
+      mw[s][g] = w;
+      den += w * ml_l[s][g];
+    }
+    for (int o = 32; o > 0; o >>= 1) den += __shfl_xor(den, o);
+    if (lane == 0) cl[g] = den;
+  }
+  __syncthreads();
+  // weighted sum of the S partial rows: wave w takes rows s = w, w + 4, ...; lane owns floats
+  // o = lane + 64 j of the GRP x 128 row (one coalesced 256-B load per wave and j)
+  {
+    constexpr int J = GRP * kD / 64;
+    float acc[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = 0.f;
+    const float* pb = part_o + (int64_t)bh * S * GRP * kD + lane;
+    for (int s = wave; s < S; s += kWaves) {
+      float x[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) x[j] = part_load(pb + (int64_t)s * GRP * kD + 64 * j);
+#pragma unroll
+      for (int j = 0; j < J; ++j) acc[j] = fmaf(mw[s][(64 * j + lane) / kD], x[j], acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) po[wave][lane + 64 * j] = acc[j];
+  }
+  __syncthreads();
+  for (int o = tid; o < GRP * kD; o += kThreads)
+    ob[o] = (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD];
+  if (tid == 0) counters[bh] = 0;  // ready for the next launch (graph replay)
 }
 
 }  // namespace
 
+extern "C" int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L) {
+  if (B < 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv || L <= 0 || L > kMaxL) return -1;
+  if (B == 0) return 0;
+  const Split sp = choose_split(B, Hkv, L);
+  const int64_t heads = B * Hkv, grp = Hq / Hkv;
+  if (sp.S == 1) return 0;
+  return heads * sp.S * grp * (kD + 2) * 4;
+}
+
 extern "C" int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v,
                                 const uint16_t* mask, float* out, int64_t B, int Hq, int Hkv,
-                                int64_t L, int D, float scale_div, void* stream) {
+                                int64_t L, int D, float scale_div, float* partials,
+                                int32_t* counters, void* stream) {
   if (!q || !k || !v || !out || B < 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv || L <= 0 ||
       L > kMaxL || D != kD || B * Hkv > 0x7fffffff)
     return QLIN_EINVAL;
   const int grp = Hq / Hkv;
   if (grp > kMaxGroup) return QLIN_EINVAL;
   if (B == 0) return QLIN_OK;
-  const dim3 grid((unsigned)(B * Hkv));
+  const Split sp = choose_split(B, Hkv, L);
+  if (sp.S > kMaxSplit || sp.S > 65535) return QLIN_EINVAL;
+  const int64_t heads = B * Hkv;
+  float *part_o = nullptr, *part_ml = nullptr;
+  if (sp.S > 1) {
+    if (!partials || !counters) return QLIN_EINVAL;
+    part_o = partials;
+    part_ml = part_o + heads * sp.S * grp * kD;
+  }
+  const dim3 grid((unsigned)heads, (unsigned)sp.S);
   hipStream_t st = (hipStream_t)stream;
-#define QLIN_A(G)                                                                          \
-  hipLaunchKernelGGL((attn_decode_kernel<G>), grid, dim3(kThreads), 0, st, q,              \
-                     (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out, Hq, \
-                     Hkv, (int)L, scale_div)
+#define QLIN_A(G)                                                                             \
+  hipLaunchKernelGGL((attn_decode_kernel<G>), grid, dim3(kThreads), 0, st, q,                 \
+                     (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out, Hq,    \
+                     Hkv, (int)L, sp.chunk, sp.S, scale_div, (int*)counters, part_o, part_ml)
   switch (grp) {
     case 1: QLIN_A(1); break;
     case 2: QLIN_A(2); break;

@@ -44,7 +44,8 @@ SIGNATURES = {
     "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
-    "qlin_attn_decode": ([_p, _p, _p, _p, _p, _l, _i, _i, _l, _i, ctypes.c_float, _p], _i),
+    "qlin_attn_decode_partials_bytes": ([_l, _i, _i, _l], _l),
+    "qlin_attn_decode": ([_p, _p, _p, _p, _p, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p], _i),
 }
 
 
@@ -278,6 +279,20 @@ def attn_decode_supported(q, k, mask=None):
             and (mask is None or (mask.dtype == torch.float16 and mask.shape[-2] == 1)))
 
 
+_ATTN_COUNTERS = {}
+
+
+def _attn_counters(device, heads):
+    """Zero-filled split-L merge counters, one buffer per (device, stream), grown on demand (the
+    kernel leaves them zero).  Grow outside graph capture: an eager call before capture sizes it."""
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    c = _ATTN_COUNTERS.get(key)
+    if c is None or c.numel() < heads:
+        c = torch.zeros(max(heads, 4096), dtype=torch.int32, device=device)
+        _ATTN_COUNTERS[key] = c
+    return c
+
+
 def attn_decode(q, k, v, mask, scale_div):
     """softmax(q k^T / scale_div + mask) v for one query token: q fp32 [B, Hq, 1, D], k/v fp16
     [B, Hkv, L, D], mask fp16 [B, 1, 1, L] or None -> fp32 [B, Hq, 1, D]."""
@@ -293,7 +308,16 @@ def attn_decode(q, k, v, mask, scale_div):
         m = mask.reshape(B, L).contiguous() if mask.shape[0] == B else \
             mask.expand(B, 1, 1, L).reshape(B, L).contiguous()
     out = torch.empty(B, Hq, 1, D, dtype=torch.float32, device=q.device)
-    rc = load_library().qlin_attn_decode(_ptr(q.contiguous()), _ptr(k), _ptr(v), _ptr(m), _ptr(out),
-                                         B, Hq, Hkv, L, D, float(scale_div), _stream(q))
+    lib = load_library()
+    nbytes = lib.qlin_attn_decode_partials_bytes(B, Hq, Hkv, L)
+    if nbytes < 0:
+        raise ValueError("attn_decode: unsupported shapes")
+    part = cnt = None
+    if nbytes:
+        part = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
+        cnt = _attn_counters(q.device, B * Hkv)
+    rc = lib.qlin_attn_decode(_ptr(q.contiguous()), _ptr(k), _ptr(v), _ptr(m), _ptr(out),
+                              B, Hq, Hkv, L, D, float(scale_div), _ptr(part), _ptr(cnt),
+                              _stream(q))
     _check(rc, "qlin_attn_decode")
     return out

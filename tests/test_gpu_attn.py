@@ -26,7 +26,8 @@ def _ref(q, k, v, mask):
 
 
 @pytest.mark.parametrize("B,Hq,Hkv,L", [(1, 32, 8, 513), (1, 32, 8, 1), (2, 8, 8, 77),
-                                        (1, 16, 2, 4096), (3, 4, 4, 300), (1, 64, 8, 1000)])
+                                        (1, 16, 2, 4096), (3, 4, 4, 300), (1, 64, 8, 1000),
+                                        (40, 32, 8, 4096), (2, 32, 8, 31), (1, 8, 8, 2049)])
 @pytest.mark.parametrize("masked", [False, True])
 def test_attn_decode_matches_reference(B, Hq, Hkv, L, masked):
     g = torch.Generator(device="cuda").manual_seed(B * 1000 + L)
@@ -41,6 +42,30 @@ def test_attn_decode_matches_reference(B, Hq, Hkv, L, masked):
     ref = _ref(q, k, v, mask)
     err = (out.double() - ref).abs().max().item()
     assert err <= 1e-5 * max(1.0, ref.abs().max().item()), err
+
+
+def test_attn_decode_split_counters_reset_under_graph_replay():
+    """The split-L merge counts blocks in on a workspace counter that the last block resets: back
+    to back eager calls and graph replays must give the same result every time."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    q = torch.randn(1, 32, 1, 128, device="cuda", generator=g)
+    k = torch.randn(1, 8, 1500, 128, device="cuda", generator=g).half()
+    v = torch.randn(1, 8, 1500, 128, device="cuda", generator=g).half()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        first = qlin.attn_decode(q, k, v, None, math.sqrt(128))
+        again = qlin.attn_decode(q, k, v, None, math.sqrt(128))
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            out = qlin.attn_decode(q, k, v, None, math.sqrt(128))
+        for _ in range(3):
+            gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(first, again)
+    assert torch.equal(first, out)
+    ref = _ref(q, k, v, None)
+    assert (first.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
 def test_attn_decode_rejects_unsupported():
