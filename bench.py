@@ -33,6 +33,12 @@ WORKLOADS = {
                        "LLaMA3-8B int4 g128 dequant-GEMV batch=1 (configs[1]), 4096x4096"),
     "gemv_int3_g64": (1, 4096, 4096, 3, 64, 64, "gemv", "int3 g64 sub-byte GEMV (configs[3])"),
     "gemv_int2_g64": (1, 4096, 4096, 2, 64, 96, "gemv", "int2 g64 sub-byte GEMV (configs[3])"),
+    "gemv_int3_g64_hqq": (1, 4096, 4096, 3, 64, 64, "gemv",
+                          "int3 g64 GEMV, HQQ fp16 zero points (QLIN_FLOAT_ZERO, configs[3])"),
+    "gemv_int2_g64_hqq": (1, 4096, 4096, 2, 64, 96, "gemv",
+                          "int2 g64 GEMV, HQQ fp16 zero points (QLIN_FLOAT_ZERO, configs[3])"),
+    "gemm_int4_g64_hqq_m2048": (2048, 4096, 4096, 4, 64, 4, "gemm",
+                                "int4 g64 HQQ fp16 zero points, one 2048-token window"),
     "gemm_int4_g128_m32": (32, 4096, 4096, 4, 128, 64, "linear",
                            "int4 g128, 32 tokens (qlin_linear_f16 dispatch: GEMV kernel x2)"),
     "gemm_int4_g128_m2048": (2048, 4096, 4096, 4, 128, 4, "gemm",
@@ -148,6 +154,11 @@ def main():
         gen.manual_seed(1_000_003 * rank + i)
         w = torch.empty(N, K, device=dev, dtype=torch.float16).normal_(0.0, 0.02, generator=gen)
         o = qlin.quantize(w, bits, group, 0, want_xdq=False, want_params=False, pack=True)
+        if args.workload.endswith("_hqq") or "_hqq_" in args.workload:
+            # HQQ-style non-integral zero points: same codes and bytes, fp16 zero in the qsz word
+            sc, zi = qlin.split_sz(o["qsz"], N)
+            o["qsz"] = qlin.join_sz_float(sc, zi.to(torch.float16) + 0.375)
+            o["flags"] = qlin.FLOAT_ZERO
         mats.append((o["qweight"], o["qsz"], o["flags"]))
         del w, o
     gen.manual_seed(1234)

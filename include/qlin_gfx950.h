@@ -29,6 +29,9 @@
  *            coalesced load gives a tile's 16 rows their group parameters.
  *   flags    QLIN_WIDE_ZERO when some |zero| > 1024 (possible only for degenerate groups: the
  *            reference clamps zero points to +-1e4), selecting the fp32 (u - zero) path.
+ *            QLIN_FLOAT_ZERO: bits 16..31 of qsz hold an fp16 zero instead (HQQ checkpoints,
+ *            whose zero points are not integral); W = RN16(RN16(u - zero) * scale), hqq's
+ *            ((W_q - zero) * scale) in fp16.
  *   group    multiple of 32 dividing K (group = K for per-channel); K % 32 == 0.
  * Both arrays must be allocated padded (ceil(N/16)*16 rows, ceil(K/128)*128 codes) and zeroed
  * before packing; the packers write rows < N only.
@@ -42,14 +45,15 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 2
+#define QLIN_ABI_VERSION 3
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
 #define QLIN_DISABLE_ZERO_POINT 2
 #define QLIN_LWC                4
-/* packed-layout flag (dequant / GEMV / GEMM entry points) */
+/* packed-layout flags (dequant / GEMV / GEMM entry points) */
 #define QLIN_WIDE_ZERO          8
+#define QLIN_FLOAT_ZERO        16
 
 /* element dtypes */
 #define QLIN_F16 0
@@ -99,6 +103,16 @@ int qlin_fake_quant(const void* x, int dtype, const void* scale, const void* zp,
 int qlin_pack_f16(const uint16_t* w_dq, const uint16_t* scales_ref, const uint16_t* zeros_ref,
                   int64_t N, int64_t K, int bits, int group, int flags,
                   uint32_t* qweight, uint32_t* qsz, void* stream);
+
+/*
+ * Integer codes -> canonical qweight, for converters whose zero points are not integral (HQQ):
+ *   codes uint8 [N, K] row-major, each < 2^bits (higher bits are ignored); qweight allocated and
+ *   zeroed as above.  The matching qsz is plain data (scale | zero << 16) built by the caller.
+ * Replaces the packing half of hqq's BaseQuantizeConfig / HQQLinear path (reference
+ * quantizehqq.py:40-49; hqq.core.bitpack pack_4bit_u8 / pack_3bit_32 / pack_2bit_u8).
+ */
+int qlin_pack_codes(const uint8_t* codes, int64_t N, int64_t K, int bits, uint32_t* qweight,
+                    void* stream);
 
 /*
  * Dequantize the canonical layout: w[n,k] = RN16(RN16(q - zp) * s), bit-exact with the reference

@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/qlin_gfx950.h"
+
 namespace qlin {
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -184,18 +186,27 @@ __device__ __forceinline__ uint32_t sz_pack(_Float16 s, int z) {
   return (uint32_t)__builtin_bit_cast(uint16_t, s) | ((uint32_t)(uint16_t)(int16_t)z << 16);
 }
 
+// zero-point modes of a packed matrix (layout flags, include/qlin_gfx950.h):
+//   kZNarrow  int16 zero, |zp| <= 1024: (off + u) - (off + zp) is the exact integer u - zp
+//   kZWide    int16 zero, |zp| > 1024 somewhere (QLIN_WIDE_ZERO): u - zp formed in fp32
+//   kZFloat   fp16 zero (QLIN_FLOAT_ZERO, HQQ checkpoints): u - zp rounded once in fp16, as
+//             hqq's ((W_q - zero) * scale) in the compute dtype
+constexpr int kZNarrow = 0;
+constexpr int kZWide = 1;
+constexpr int kZFloat = 2;
+
 // per-group dequant constants for the exact path
 struct GroupQ {
   h2 ss;     // (s, s)
-  h2 zz[4];  // (off_P + zp) pairs, narrow zeros
+  h2 zz[4];  // (off_P + zp) pairs, narrow zeros; (zp, zp) in zz[0], float zeros
   float zf;  // zp, wide zeros
 };
 
-template <int BITS, bool WIDE>
+template <int BITS, int ZM>
 __device__ __forceinline__ GroupQ make_group(_Float16 s, int zp) {
   GroupQ g;
   g.ss = h2{s, s};
-  if constexpr (!WIDE) {
+  if constexpr (ZM == kZNarrow) {
 #pragma unroll
     for (int P = 0; P < 4; ++P) {
       const _Float16 z = (_Float16)(pair_off<BITS>(P) + zp);  // exact: |zp| <= 1024
@@ -209,20 +220,26 @@ __device__ __forceinline__ GroupQ make_group(_Float16 s, int zp) {
 
 // the same straight from a qsz word, in fp16 arithmetic: int16 -> fp16 is exact for |zp| <= 2048
 // and off + zp is exact for |zp| <= 1024 (narrow), so no int -> fp32 -> fp16 round trip
-template <int BITS, bool WIDE>
+template <int BITS, int ZM>
 __device__ __forceinline__ GroupQ make_group_w(uint32_t w) {
-  if constexpr (WIDE) return make_group<BITS, true>(sz_scale(w), sz_zero(w));
+  if constexpr (ZM == kZWide) return make_group<BITS, kZWide>(sz_scale(w), sz_zero(w));
   GroupQ g;
   const _Float16 s = sz_scale(w);
-  const _Float16 z = (_Float16)(int16_t)(w >> 16);
   g.ss = h2{s, s};
+  if constexpr (ZM == kZFloat) {
+    const _Float16 z = __builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+    g.zz[0] = h2{z, z};
+  } else {
+    const _Float16 z = (_Float16)(int16_t)(w >> 16);
 #pragma unroll
-  for (int P = 0; P < 4; ++P) g.zz[P] = h2{z, z} + h2{(_Float16)pair_off<BITS>(P), (_Float16)pair_off<BITS>(P)};
+    for (int P = 0; P < 4; ++P)
+      g.zz[P] = h2{z, z} + h2{(_Float16)pair_off<BITS>(P), (_Float16)pair_off<BITS>(P)};
+  }
   return g;
 }
 
 // exact dequantized fp16 values of k-step S: out[P] = (w_2P, w_2P+1) = RN16(RN16(u - zp) * s)
-template <int BITS, bool WIDE, int S>
+template <int BITS, int ZM, int S>
 __device__ __forceinline__ void dequant_step(const Piece<BITS>& c, const Magics& mg, const GroupQ& g,
                                              uint32_t (&out)[4]) {
 #pragma clang fp contract(off)
@@ -232,8 +249,12 @@ __device__ __forceinline__ void dequant_step(const Piece<BITS>& c, const Magics&
   for (int P = 0; P < 4; ++P) {
     const h2 q = as_h2(v[P]);
     h2 d;
-    if constexpr (!WIDE) {
+    if constexpr (ZM == kZNarrow) {
       d = q - g.zz[P];  // exact integer u - zp
+    } else if constexpr (ZM == kZFloat) {
+      // (off + u) - off is the exact code u; minus the fp16 zero rounds once (hqq: W_q - zero)
+      const _Float16 off = (_Float16)pair_off<BITS>(P);
+      d = (q - h2{off, off}) - g.zz[0];
     } else {
       // |zp| > 1024 (up to 1e4, QLIN_WIDE_ZERO): u - zp formed exactly in fp32, rounded once to
       // fp16 as the reference's fp16 x_int.sub(round_zero_point) does
@@ -265,6 +286,12 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 }  // namespace qlin
+
+// zero mode from the layout flags (QLIN_FLOAT_ZERO wins: an fp16 zero is never "wide")
+__host__ __device__ inline int zero_mode(int flags) {
+  return (flags & QLIN_FLOAT_ZERO) ? qlin::kZFloat
+         : (flags & QLIN_WIDE_ZERO) ? qlin::kZWide : qlin::kZNarrow;
+}
 
 // error codes (hipError_t values)
 #define QLIN_OK 0

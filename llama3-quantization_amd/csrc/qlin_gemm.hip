@@ -133,7 +133,7 @@ __device__ __forceinline__ void read_a(h8 (&a)[MB], const unsigned char* as, int
 }
 
 // FULL: every k-tile lies inside K (K % 128 == 0, chosen per launch): straight-line k-steps
-template <int BITS, bool WN_, int GPT, bool WIDE, bool FULL>
+template <int BITS, bool WN_, int GPT, int ZM, bool FULL>
 __device__ __forceinline__ void compute_stage(const unsigned char* st, const GemmGeo& g, int kt,
                                               f4 (&acc)[Cfg<BITS, WN_>::MB][Cfg<BITS, WN_>::NB]) {
   using C = Cfg<BITS, WN_>;
@@ -165,7 +165,7 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const uint32_t sw = ss[((wn * NB + nb) * GPT + slot) * 16 + n_in];
-      gq[nb] = make_group_w<BITS, WIDE>(sw);
+      gq[nb] = make_group_w<BITS, ZM>(sw);
     }
   };
 
@@ -181,7 +181,7 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       uint32_t v[4];
-      dequant_step<BITS, WIDE, S>(pc[nb], mg, gq[nb], v);
+      dequant_step<BITS, ZM, S>(pc[nb], mg, gq[nb], v);
       const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
@@ -196,7 +196,7 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 
 // ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
 // the DMA after the first k-tile; the library instantiates ABL = 0 only
-template <int BITS, bool WN_, int GPT, bool WIDE, bool KFULL, int ABL = 0>
+template <int BITS, bool WN_, int GPT, int ZM, bool KFULL, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(
     if (!(ABL & 2) && kt + 1 < g.Kt)
       load_stage<BITS, WN_, GPT>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
     if (!(ABL & 1))
-      compute_stage<BITS, WN_, GPT, WIDE, KFULL>(smem + (kt & 1) * C::STAGE, g, kt, acc);
+      compute_stage<BITS, WN_, GPT, ZM, KFULL>(smem + (kt & 1) * C::STAGE, g, kt, acc);
   }
 
   // epilogue: lane (n, q) holds C[4q + i][n] of each 16 x 16 block
@@ -265,7 +265,7 @@ uint32_t group_magic(int group) {
   return (uint32_t)(((1ull << 31) + d - 1) / d);
 }
 
-template <int BITS, bool WN_, int GPT, bool WIDE>
+template <int BITS, bool WN_, int GPT, int ZM>
 int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
   const int tiles_n = (N + Cfg<BITS, WN_>::BN - 1) / Cfg<BITS, WN_>::BN;
@@ -273,7 +273,7 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   const int64_t blocks = tiles_m * tiles_n;
   if (blocks > 0x7fffffff) return QLIN_EINVAL;
 #define QLIN_GL(KF)                                                                           \
-  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, WIDE, KF>), dim3((unsigned)blocks),           \
+  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, ZM, KF>), dim3((unsigned)blocks),           \
                      dim3(kThreads), 0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, \
                      (_Float16*)y, M, N, K, group, group_magic(group), (int)tiles_m, tiles_n)
   // straight-line k-steps need K % 128 == 0; the wide tile with 2-4 group slots per k-tile then
@@ -286,23 +286,23 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
 
 constexpr int64_t kWideMinBlocks = 512;  // >= 2 blocks per CU on 256 CUs
 
-template <int BITS, int GPT, bool WIDE>
+template <int BITS, int GPT, int ZM>
 int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                 uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
   if constexpr (BITS != 8) {
     const int64_t wide_blocks = ((M + BM - 1) / BM) * ((N + 511) / 512);
     if (wide_blocks >= kWideMinBlocks)
-      return launch_gemm_t<BITS, true, GPT, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+      return launch_gemm_t<BITS, true, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
   }
-  return launch_gemm_t<BITS, false, GPT, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  return launch_gemm_t<BITS, false, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
 }
 
-template <int BITS, bool WIDE>
+template <int BITS, int ZM>
 int launch_gemm_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
-  if (group % 128 == 0) return launch_gemm<BITS, 1, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
-  if (group % 64 == 0) return launch_gemm<BITS, 2, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
-  return launch_gemm<BITS, 4, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (group % 128 == 0) return launch_gemm<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (group % 64 == 0) return launch_gemm<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+  return launch_gemm<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
 }
 
 bool valid(int64_t M, int64_t N, int64_t K, int bits, int group) {
@@ -321,11 +321,12 @@ extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int f
   if (!qweight || !qsz || !x || !y || !valid(M, N, K, bits, group)) return QLIN_EINVAL;
   if (M == 0 || N == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
-  const bool wide = flags & QLIN_WIDE_ZERO;
+  const int zm = zero_mode(flags);
   const int n = (int)N, k = (int)K;
-#define QLIN_M(B)                                                                     \
-  return wide ? launch_gemm_g<B, true>(qweight, qsz, x, bias, y, M, n, k, group, st) \
-              : launch_gemm_g<B, false>(qweight, qsz, x, bias, y, M, n, k, group, st)
+#define QLIN_M(B)                                                                              \
+  return zm == kZFloat  ? launch_gemm_g<B, kZFloat>(qweight, qsz, x, bias, y, M, n, k, group, st) \
+         : zm == kZWide ? launch_gemm_g<B, kZWide>(qweight, qsz, x, bias, y, M, n, k, group, st)  \
+                        : launch_gemm_g<B, kZNarrow>(qweight, qsz, x, bias, y, M, n, k, group, st)
   switch (bits) {
     case 2: QLIN_M(2);
     case 3: QLIN_M(3);

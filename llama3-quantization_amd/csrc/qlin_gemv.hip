@@ -114,7 +114,7 @@ __device__ __forceinline__ void park_x(h8 (&xa)[4], const XRaw<MT>& r, uint32_t*
   for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, b[4 * s]);
 }
 
-template <int BITS, int MT, int GPT, bool WIDE, int PF>
+template <int BITS, int MT, int GPT, int ZM, int PF>
 __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0, int nts,
                                           int ktl, f4& acc) {
   const Magics mg = make_magics<BITS>();
@@ -127,8 +127,8 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
     const int k0 = kt * kTileK + 32 * S;
     if (FULL || k0 < g.K) {  // wave-uniform
       uint32_t v[4];
-      const GroupQ gq = make_group_w<BITS, WIDE>(t.sz[slot]);
-      dequant_step<BITS, WIDE, S>(t.pc, mg, gq, v);
+      const GroupQ gq = make_group_w<BITS, ZM>(t.sz[slot]);
+      dequant_step<BITS, ZM, S>(t.pc, mg, gq, v);
       const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, acc, 0, 0, 0);
     }
@@ -175,7 +175,7 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
 
 }
 
-template <int BITS, int MT, int GPT, bool WIDE, int PF>
+template <int BITS, int MT, int GPT, int ZM, int PF>
 __global__ __launch_bounds__(1024) void gemv_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
   const int ktl = max(0, min(Kt - 1, kt0 + nts - 1));
 
   f4 acc = {0.f, 0.f, 0.f, 0.f};
-  gemv_body<BITS, MT, GPT, WIDE, PF>(g, &xs[wave][0], kt0, nts, ktl, acc);
+  gemv_body<BITS, MT, GPT, ZM, PF>(g, &xs[wave][0], kt0, nts, ktl, acc);
 
   // combine the W partials of each (row m < MT, column n): C row m = 4q + i sits in lane
   // n + 16q, element i; layout [m][n][wave] so one thread reads its 16 partials with 4
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
 }
 
 // standalone exact dequant: one thread per lane piece -> 4 x 8 fp16 values of one row
-template <int BITS, bool WIDE>
+template <int BITS, int ZM>
 __global__ __launch_bounds__(256) void dequant_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz, _Float16* __restrict__ w,
     int64_t total_pieces, int N, int K, int group) {
@@ -260,9 +260,9 @@ __global__ __launch_bounds__(256) void dequant_kernel(
     const int k0 = kt * kTileK + 32 * S + 8 * q;
     if (k0 >= K) return;
     const uint32_t sw = qsz[sz_index(nt, k0 / group, G, n_in)];
-    const GroupQ g = make_group_w<BITS, WIDE>(sw);
+    const GroupQ g = make_group_w<BITS, ZM>(sw);
     uint32_t o[4];
-    dequant_step<BITS, WIDE, S>(c, mg, g, o);
+    dequant_step<BITS, ZM, S>(c, mg, g, o);
     *reinterpret_cast<uint4*>(w + row * K + k0) = make_uint4(o[0], o[1], o[2], o[3]);
   };
   one(std::integral_constant<int, 0>{});
@@ -290,7 +290,7 @@ int pick_waves(int Nt, int Kt, int& tpw) {
   return (Kt + tpw - 1) / tpw;
 }
 
-template <int BITS, int MT, int GPT, bool WIDE>
+template <int BITS, int MT, int GPT, int ZM>
 int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
   const int Nt = (N + kTileN - 1) / kTileN;
@@ -299,7 +299,7 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   const int W = pick_waves(Nt, Kt, tpw);
   const uint32_t gs = group_magic(group);
 #define QLIN_GV(PF)                                                                        \
-  hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, WIDE, PF>), dim3(Nt), dim3(64 * W), \
+  hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, ZM, PF>), dim3(Nt), dim3(64 * W), \
                      0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias,             \
                      (_Float16*)y, M, N, K, group, gs, tpw)
   if constexpr (MT >= 8) {  // x registers of 4 tiles in flight would spill
@@ -312,24 +312,24 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   return (int)hipGetLastError();
 }
 
-template <int BITS, int MT, bool WIDE>
+template <int BITS, int MT, int ZM>
 int launch_gemv_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
   if (group % 128 == 0)
-    return launch_gemv<BITS, MT, 1, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+    return launch_gemv<BITS, MT, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
   if (group % 64 == 0)
-    return launch_gemv<BITS, MT, 2, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
-  return launch_gemv<BITS, MT, 4, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+    return launch_gemv<BITS, MT, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+  return launch_gemv<BITS, MT, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
 }
 
-template <int BITS, bool WIDE>
+template <int BITS, int ZM>
 int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
-  if (M == 1) return launch_gemv_g<BITS, 1, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
-  if (M == 2) return launch_gemv_g<BITS, 2, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
-  if (M <= 4) return launch_gemv_g<BITS, 4, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
-  if (M <= 8) return launch_gemv_g<BITS, 8, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
-  return launch_gemv_g<BITS, 16, WIDE>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (M == 1) return launch_gemv_g<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (M == 2) return launch_gemv_g<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (M <= 4) return launch_gemv_g<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+  if (M <= 8) return launch_gemv_g<BITS, 8, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+  return launch_gemv_g<BITS, 16, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
 }
 
 }  // namespace
@@ -341,14 +341,14 @@ extern "C" int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, in
   if (pieces == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)((pieces + 255) / 256));
-  const bool wide = flags & QLIN_WIDE_ZERO;
+  const int zm = zero_mode(flags);
+#define QLIN_D1(B, Z)                                                                          \
+  hipLaunchKernelGGL((dequant_kernel<B, Z>), grid, dim3(256), 0, st, qweight, qsz,             \
+                     (_Float16*)w, pieces, (int)N, (int)K, group)
 #define QLIN_D(B)                                                                              \
-  if (wide)                                                                                    \
-    hipLaunchKernelGGL((dequant_kernel<B, true>), grid, dim3(256), 0, st, qweight, qsz,        \
-                       (_Float16*)w, pieces, (int)N, (int)K, group);                           \
-  else                                                                                         \
-    hipLaunchKernelGGL((dequant_kernel<B, false>), grid, dim3(256), 0, st, qweight, qsz,       \
-                       (_Float16*)w, pieces, (int)N, (int)K, group);                           \
+  if (zm == kZFloat) QLIN_D1(B, kZFloat);                                                      \
+  else if (zm == kZWide) QLIN_D1(B, kZWide);                                                   \
+  else QLIN_D1(B, kZNarrow);                                                                   \
   break
   switch (bits) {
     case 2: QLIN_D(2);
@@ -357,6 +357,7 @@ extern "C" int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, in
     default: QLIN_D(8);
   }
 #undef QLIN_D
+#undef QLIN_D1
   return (int)hipGetLastError();
 }
 
@@ -368,10 +369,11 @@ extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int f
   if (N == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
   const int m = (int)M, n = (int)N, k = (int)K;
-#define QLIN_G(B)                                                                         \
-  return (flags & QLIN_WIDE_ZERO)                                                         \
-             ? launch_gemv_m<B, true>(qweight, qsz, x, bias, y, m, n, k, group, st) \
-             : launch_gemv_m<B, false>(qweight, qsz, x, bias, y, m, n, k, group, st)
+  const int zm = zero_mode(flags);
+#define QLIN_G(B)                                                                           \
+  return zm == kZFloat  ? launch_gemv_m<B, kZFloat>(qweight, qsz, x, bias, y, m, n, k, group, st) \
+         : zm == kZWide ? launch_gemv_m<B, kZWide>(qweight, qsz, x, bias, y, m, n, k, group, st)  \
+                        : launch_gemv_m<B, kZNarrow>(qweight, qsz, x, bias, y, m, n, k, group, st)
   switch (bits) {
     case 2: QLIN_G(2);
     case 3: QLIN_G(3);

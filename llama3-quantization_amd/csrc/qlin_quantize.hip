@@ -280,6 +280,34 @@ __global__ __launch_bounds__(kThreads) void fq_kernel(
     pack_piece<BITS>(u, qweight + piece_off(row >> 4, kt, Kt, (int)(row & 15) + 16 * q, BITS));
 }
 
+// integer codes -> tiled qweight: one thread per lane piece gathers its 32 codes (four 8-byte
+// runs of one row) and packs them (converters whose zero points are not integral, e.g. HQQ's
+// fp16 zeros, cannot recover codes from W_dq as qlin_pack_f16 does)
+template <int BITS>
+__global__ __launch_bounds__(kThreads) void pack_codes_kernel(const uint8_t* __restrict__ codes,
+                                                              int64_t pieces, int N, int K,
+                                                              uint32_t* __restrict__ qweight) {
+  const int64_t pc = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (pc >= pieces) return;
+  const int Kt = (K + kTileK - 1) / kTileK;
+  const int lane = (int)(pc & 63);
+  const int64_t tt = pc >> 6;
+  const int kt = (int)(tt % Kt);
+  const int64_t row = (tt / Kt) * kTileN + (lane & 15);
+  const int q = lane >> 4;
+  constexpr uint32_t mask = (1u << BITS) - 1u;
+  uint32_t u[32];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = kt * kTileK + 32 * s + 8 * q;  // K % 32 == 0: a run is wholly in or out
+    uint2 r = make_uint2(0u, 0u);
+    if (row < N && k < K) r = *reinterpret_cast<const uint2*>(codes + row * K + k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) u[8 * s + j] = ((j < 4 ? r.x : r.y) >> (8 * (j & 3))) & mask;
+  }
+  pack_piece<BITS>(u, qweight + pc * BITS);
+}
+
 template <typename T>
 int launch_quantize(const void* x, int64_t rows, int64_t K, int bits, int group, int flags,
                     const void* up, const void* low, void* x_dq, void* scale_out, void* zp_out,
@@ -383,4 +411,27 @@ extern "C" int qlin_pack_f16(const uint16_t* w_dq, const uint16_t* scales_ref,
   if (!w_dq || !qweight || !qsz) return QLIN_EINVAL;
   return qlin_fake_quant(w_dq, QLIN_F16, scales_ref, zeros_ref, N, K, bits, group, flags, nullptr,
                          qweight, qsz, stream);
+}
+
+extern "C" int qlin_pack_codes(const uint8_t* codes, int64_t N, int64_t K, int bits,
+                               uint32_t* qweight, void* stream) {
+  if (!codes || !qweight || N < 0 || N > (1 << 30) || K <= 0 || K % 32 || K > (1 << 20) ||
+      !(bits == 2 || bits == 3 || bits == 4 || bits == 8))
+    return QLIN_EINVAL;
+  const int64_t pieces = ((N + kTileN - 1) / kTileN) * ((K + kTileK - 1) / kTileK) * 64;
+  if (pieces == 0) return QLIN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)((pieces + kThreads - 1) / kThreads));
+#define QLIN_PC(B)                                                                             \
+  hipLaunchKernelGGL((pack_codes_kernel<B>), grid, dim3(kThreads), 0, st, codes, pieces,       \
+                     (int)N, (int)K, qweight);                                                 \
+  break
+  switch (bits) {
+    case 2: QLIN_PC(2);
+    case 3: QLIN_PC(3);
+    case 4: QLIN_PC(4);
+    default: QLIN_PC(8);
+  }
+#undef QLIN_PC
+  return (int)hipGetLastError();
 }

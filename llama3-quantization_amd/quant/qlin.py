@@ -16,12 +16,13 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
 LWC = 4
 WIDE_ZERO = 8
+FLOAT_ZERO = 16
 F16 = 0
 F32 = 1
 
@@ -40,6 +41,7 @@ SIGNATURES = {
     "qlin_quantize": ([_p, _i, _l, _l, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p], _i),
     "qlin_fake_quant": ([_p, _i, _p, _p, _l, _l, _i, _i, _i, _p, _p, _p, _p], _i),
     "qlin_pack_f16": ([_p, _p, _p, _l, _l, _i, _i, _i, _p, _p, _p], _i),
+    "qlin_pack_codes": ([_p, _l, _l, _i, _p, _p], _i),
     "qlin_dequant_f16": ([_p, _p, _i, _l, _l, _i, _i, _p, _p], _i),
     "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
@@ -150,6 +152,30 @@ def join_sz(scales: torch.Tensor, zeros: torch.Tensor) -> torch.Tensor:
     w = torch.zeros(nt * TILE_N, G, dtype=torch.int32, device=scales.device)
     w[:N] = lo | hi
     return w.view(nt, TILE_N, G).permute(0, 2, 1).contiguous()
+
+
+def join_sz_float(scales: torch.Tensor, zeros: torch.Tensor) -> torch.Tensor:
+    """(scales fp16 [N, G], zeros fp16 [N, G]) -> qsz [ceil(N/16), G, 16] with the fp16 zero in
+    the high half (layout flag QLIN_FLOAT_ZERO; HQQ's non-integral zero points)."""
+    N, G = scales.shape
+    nt = -(-N // TILE_N)
+    lo = scales.to(torch.float16).contiguous().view(torch.int16).to(torch.int32) & 0xFFFF
+    hi = zeros.to(torch.float16).contiguous().view(torch.int16).to(torch.int32) << 16
+    w = torch.zeros(nt * TILE_N, G, dtype=torch.int32, device=scales.device)
+    w[:N] = lo | hi
+    return w.view(nt, TILE_N, G).permute(0, 2, 1).contiguous()
+
+
+def pack_codes(codes: torch.Tensor, bits: int) -> torch.Tensor:
+    """Integer codes uint8 [N, K] -> tiled qweight (``qlin_pack_codes``)."""
+    _dev(codes)
+    if codes.dtype != torch.uint8 or codes.dim() != 2:
+        raise ValueError(f"codes must be uint8 [N, K], got {codes.dtype} {tuple(codes.shape)}")
+    N, K = codes.shape
+    qw = torch.zeros(packed_shape(N, K, bits), dtype=torch.int32, device=codes.device)
+    rc = load_library().qlin_pack_codes(_ptr(codes), N, K, bits, _ptr(qw), _stream(codes))
+    _check(rc, "qlin_pack_codes")
+    return qw
 
 
 def sz_flags(qsz: torch.Tensor) -> int:

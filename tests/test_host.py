@@ -22,7 +22,7 @@ def test_header_declares_the_abi():
     syms = declared_symbols()
     for s in ("qlin_quantize", "qlin_fake_quant", "qlin_pack_f16", "qlin_dequant_f16",
               "qlin_gemv_f16", "qlin_gemm_f16", "qlin_linear_f16", "qlin_abi_version",
-              "qlin_error_string"):
+              "qlin_error_string", "qlin_pack_codes"):
         assert s in syms
 
 
@@ -54,6 +54,9 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert lib.qlin_gemm_f16(p, p, 0, p, None, p, 8, 16, 64, 4, 48, None, None) == 1  # group % 32
     assert lib.qlin_linear_f16(p, p, 0, p, None, p, 8, -1, 64, 4, 64, None) == 1  # N < 0
     assert lib.qlin_dequant_f16(p, p, 0, 16, 64, 3, 128, p, None) == 1  # group > K
+    assert lib.qlin_pack_codes(None, 16, 64, 4, None, None) == 1
+    assert lib.qlin_pack_codes(p, 16, 48, 4, p, None) == 1  # K % 32
+    assert lib.qlin_pack_codes(p, 16, 64, 5, p, None) == 1  # bits
     assert lib.qlin_error_string(1) == b"invalid argument"
 
 
