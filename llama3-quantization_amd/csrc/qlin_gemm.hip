@@ -28,7 +28,11 @@ using namespace qlin;
 
 namespace {
 
-constexpr int kThreads = 256;
+// 8 waves per block, side by side in N (2 per SIMD: one wave's dequant VALU and LDS reads run
+// under the other's MFMAs).  Measured against 4 waves (tools/dev/gemm_lab.py, int4 g128
+// N = K = 4096): M = 2048 narrow 923 -> 1010, M = 16384 wide 1021 -> 1135, M = 65536 wide
+// 1049 -> 1112 TFLOP/s.
+constexpr int kWaves = 8;
 constexpr int BM = 128, BK = kTileK;  // block rows; one packed k-tile per stage
 constexpr int64_t kSkinnyMaxM = 64;   // qlin_linear_f16: M <= this runs the GEMV kernel
 
@@ -40,9 +44,10 @@ typedef __attribute__((address_space(1))) void* gbl_ptr;
 // free, and the 4 waves sit side by side in N, so every B element is dequantized once per block.
 // WIDE_N: block 128 x 512 (int2/3/4 when the grid has >= 2 blocks per CU); otherwise 128 x 256
 // (twice the blocks; int8 always: twice the code bytes).
-template <int BITS, bool WIDE_N> struct Cfg {
+template <int BITS, bool WIDE_N, int NW = 4> struct Cfg {
   static constexpr int BN = WIDE_N ? 512 : 256;
-  static constexpr int WGN = 4, WGM = 1;  // the 4 waves side by side in N: B dequantized once
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int WGN = NW, WGM = 1;  // the waves side by side in N: B dequantized once
   static constexpr int WM = BM / WGM, WN = BN / WGN;
   static constexpr int MB = WM / 16, NB = WN / kTileN;  // 16 x 16 MFMA blocks per wave
   static constexpr int RT = BN / kTileN;                // packed row tiles per block
@@ -73,24 +78,24 @@ __device__ __forceinline__ int gemm_group_of(const GemmGeo& g, int k) {
 }
 
 // one k-tile's DMA into stage buffer `st`: x tile, packed codes, (scale, zero) words
-template <int BITS, bool WN_, int GPT>
+template <int BITS, bool WN_, int GPT, int NW>
 __device__ __forceinline__ void load_stage(unsigned char* st, const GemmGeo& g, int kt,
                                            const _Float16* __restrict__ x,
                                            const uint32_t* __restrict__ qw,
                                            const uint32_t* __restrict__ qsz) {
-  using C = Cfg<BITS, WN_>;
-  // x: BM rows x 16 chunks; one instruction = 4 rows (1 KB); wave w owns rows [BM/4 w, +BM/4).
+  using C = Cfg<BITS, WN_, NW>;
+  // x: BM rows x 16 chunks; one instruction = 4 rows (1 KB); wave w owns rows [BM/NW w, +BM/NW).
   // Rows >= M re-read row M-1 and k >= K re-reads the row's last chunk: those C rows are never
   // stored and those k-steps are skipped.
   {
     const int sub = g.lane >> 4, p = g.lane & 15;
 #pragma unroll
-    for (int j = 0; j < BM / 16; ++j) {
-      const int r = (BM / 4) * g.wave + 4 * j + sub;  // LDS row
+    for (int j = 0; j < BM / (4 * NW); ++j) {
+      const int r = (BM / NW) * g.wave + 4 * j + sub;  // LDS row
       const int c = p ^ (r & 15);                      // logical chunk held at physical p
       const int64_t m = min(g.m0 + r, g.M - 1);
       const int k = min(kt * BK + 8 * c, g.K - 8);
-      glds16(x + m * g.K + k, st + ((BM / 4) * g.wave + 4 * j) * 256);
+      glds16(x + m * g.K + k, st + ((BM / NW) * g.wave + 4 * j) * 256);
     }
   }
   // packed codes: RT row tiles x 256*BITS bytes, lane-linear 16-B chunks
@@ -98,7 +103,7 @@ __device__ __forceinline__ void load_stage(unsigned char* st, const GemmGeo& g, 
     constexpr int CH = C::RT * 16 * BITS;  // chunks per stage
     unsigned char* bs = st + C::A_BYTES;
 #pragma unroll
-    for (int j = g.wave; j < CH / 64; j += 4) {
+    for (int j = g.wave; j < CH / 64; j += NW) {
       const int c = 64 * j + g.lane;
       const int rt = c / (16 * BITS), o = c % (16 * BITS);
       const int64_t nt = min(g.nt0 + rt, g.ntl);
@@ -110,7 +115,7 @@ __device__ __forceinline__ void load_stage(unsigned char* st, const GemmGeo& g, 
     unsigned char* ss = st + C::A_BYTES + C::B_BYTES;
     constexpr int WORDS = C::RT * GPT * 16;
 #pragma unroll
-    for (int j = g.wave; j < WORDS / 64; j += 4) {
+    for (int j = g.wave; j < WORDS / 64; j += NW) {
       const int w = 64 * j + g.lane;
       const int rt = w / (16 * GPT), i = (w / 16) % GPT, n = w & 15;
       const int64_t nt = min(g.nt0 + rt, g.ntl);
@@ -133,10 +138,10 @@ __device__ __forceinline__ void read_a(h8 (&a)[MB], const unsigned char* as, int
 }
 
 // FULL: every k-tile lies inside K (K % 128 == 0, chosen per launch): straight-line k-steps
-template <int BITS, bool WN_, int GPT, int ZM, bool FULL>
+template <int BITS, bool WN_, int GPT, int ZM, bool FULL, int NW>
 __device__ __forceinline__ void compute_stage(const unsigned char* st, const GemmGeo& g, int kt,
-                                              f4 (&acc)[Cfg<BITS, WN_>::MB][Cfg<BITS, WN_>::NB]) {
-  using C = Cfg<BITS, WN_>;
+                                              f4 (&acc)[Cfg<BITS, WN_, NW>::MB][Cfg<BITS, WN_, NW>::NB]) {
+  using C = Cfg<BITS, WN_, NW>;
   constexpr int MB = C::MB, NB = C::NB, WM = C::WM;
   const int wm = g.wave / C::WGN, wn = g.wave % C::WGN;
   const int lane = g.lane, n_in = lane & 15, q = lane >> 4;
@@ -196,12 +201,12 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 
 // ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
 // the DMA after the first k-tile; the library instantiates ABL = 0 only
-template <int BITS, bool WN_, int GPT, int ZM, bool KFULL, int ABL = 0>
-__global__ __launch_bounds__(kThreads) void gemm_kernel(
+template <int BITS, bool WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
     int64_t M, int N, int K, int group, uint32_t gmagic, int tiles_m, int tiles_n) {
-  using C = Cfg<BITS, WN_>;
+  using C = Cfg<BITS, WN_, NW>;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * C::STAGE];
   GemmGeo g;
   g.M = M;
@@ -230,15 +235,15 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(
 #pragma unroll
     for (int j = 0; j < C::NB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  load_stage<BITS, WN_, GPT>(smem, g, 0, x, qw, qsz);
+  load_stage<BITS, WN_, GPT, NW>(smem, g, 0, x, qw, qsz);
   for (int kt = 0; kt < g.Kt; ++kt) {
     // stage kt has landed for every wave, and every wave is done reading stage kt - 1
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
     __syncthreads();
     if (!(ABL & 2) && kt + 1 < g.Kt)
-      load_stage<BITS, WN_, GPT>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
+      load_stage<BITS, WN_, GPT, NW>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
     if (!(ABL & 1))
-      compute_stage<BITS, WN_, GPT, ZM, KFULL>(smem + (kt & 1) * C::STAGE, g, kt, acc);
+      compute_stage<BITS, WN_, GPT, ZM, KFULL, NW>(smem + (kt & 1) * C::STAGE, g, kt, acc);
   }
 
   // epilogue: lane (n, q) holds C[4q + i][n] of each 16 x 16 block
@@ -273,8 +278,8 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   const int64_t blocks = tiles_m * tiles_n;
   if (blocks > 0x7fffffff) return QLIN_EINVAL;
 #define QLIN_GL(KF)                                                                           \
-  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, ZM, KF>), dim3((unsigned)blocks),           \
-                     dim3(kThreads), 0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, \
+  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, ZM, KF, 0, kWaves>), dim3((unsigned)blocks), \
+                     dim3(64 * kWaves), 0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, \
                      (_Float16*)y, M, N, K, group, group_magic(group), (int)tiles_m, tiles_n)
   // straight-line k-steps need K % 128 == 0; the wide tile with 2-4 group slots per k-tile then
   // spills (the per-step checks bound the scheduler), so it keeps the checked form

@@ -3,18 +3,22 @@
 
 extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, uint16_t* y,
                         int64_t M, int N, int K, int abl, void* stream) {
-  // abl bit 2: the wide (128 x 512) tile
+  // abl bit 2: the wide (128 x 512) tile; bit 3: 8 waves per block (else 4)
   const bool wn = abl & 4;
+  const bool w8 = abl & 8;
   const int tiles_n = (N + (wn ? 512 : 256) - 1) / (wn ? 512 : 256);
   const int tiles_m = (int)((M + BM - 1) / BM);
   const dim3 grid(tiles_m * tiles_n);
-#define L(W, A)                                                                                 \
-  hipLaunchKernelGGL((gemm_kernel<4, W, 1, false, true, A>), grid, dim3(kThreads), 0,                 \
+#define L(W, A, NW)                                                                             \
+  hipLaunchKernelGGL((gemm_kernel<4, W, 1, kZNarrow, true, A, NW>), grid, dim3(64 * NW), 0,     \
                      (hipStream_t)stream, qw, qsz, (const _Float16*)x, nullptr, (_Float16*)y, M, \
                      N, K, 128, group_magic(128), tiles_m, tiles_n)
+#define LA(W, NW) \
+  { if (a == 0) L(W, 0, NW); else if (a == 1) L(W, 1, NW); else if (a == 2) L(W, 2, NW); else L(W, 3, NW); }
   const int a = abl & 3;
-  if (wn) { if (a == 0) L(true, 0); else if (a == 1) L(true, 1); else if (a == 2) L(true, 2); else L(true, 3); }
-  else { if (a == 0) L(false, 0); else if (a == 1) L(false, 1); else if (a == 2) L(false, 2); else L(false, 3); }
+  if (w8) { if (wn) LA(true, 8) else LA(false, 8) }
+  else { if (wn) LA(true, 4) else LA(false, 4) }
+#undef LA
 #undef L
   return (int)hipGetLastError();
 }
