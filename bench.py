@@ -77,6 +77,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="gemv_int4_g128", choices=sorted(WORKLOADS))
     ap.add_argument("--ring", type=int, default=None)
+    ap.add_argument("--split", action="store_true",
+                    help="strong scaling: every rank streams rows [r*N/P, (r+1)*N/P) of the SAME "
+                         "ring (output-feature sharding, SURVEY.md §8(e)); default: weak scaling, "
+                         "an independent ring per rank")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -145,14 +149,22 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    M, N, K, bits, group, ring, kernel, note = WORKLOADS[args.workload]
+    M, N_full, K, bits, group, ring, kernel, note = WORKLOADS[args.workload]
+    N = N_full
+    row0 = 0
+    if args.split and world > 1:
+        # output-feature shard, whole 16-row tiles: the packed layout of a row range is contiguous
+        tiles = -(-N_full // 16)
+        t0, t1 = tiles * rank // world, tiles * (rank + 1) // world
+        row0, N = 16 * t0, min(N_full, 16 * t1) - 16 * t0
     R = args.ring or ring
     gen = torch.Generator(device=dev)
     mats = []
     zb = 2
     for i in range(R):
-        gen.manual_seed(1_000_003 * rank + i)
-        w = torch.empty(N, K, device=dev, dtype=torch.float16).normal_(0.0, 0.02, generator=gen)
+        gen.manual_seed((0 if args.split else 1_000_003 * rank) + i)
+        w = torch.empty(N_full, K, device=dev, dtype=torch.float16).normal_(0.0, 0.02, generator=gen)
+        w = w[row0:row0 + N].contiguous()
         o = qlin.quantize(w, bits, group, 0, want_xdq=False, want_params=False, pack=True)
         if args.workload.endswith("_hqq") or "_hqq_" in args.workload:
             # HQQ-style non-integral zero points: same codes and bytes, fp16 zero in the qsz word
@@ -227,7 +239,9 @@ def main():
     nbytes = algo_bytes(M, N, K, bits, group)
     read_bytes = algo_bytes(M, N, K, bits, group, zb)
     per_launch_s = elapsed / launches
-    value = flops * launches * world / elapsed / 1e12
+    # whole job: weak = every rank's full ring; strong = the one shared ring (rows summed)
+    job_flops = 2.0 * M * N_full * K if args.split else flops * world
+    value = job_flops * launches / elapsed / 1e12
     hbm_bound = kernel in ("gemv", "linear") or M <= 256
     if hbm_bound:
         roof = {"bound": "hbm", "achieved": round(nbytes / per_launch_s / 1e9, 1),
@@ -257,14 +271,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.split else "weak",
         "vs_baseline": None,
         "dtype": "f16",
         "data": "synthetic",
         "hbm_GBps_total": round(nbytes * launches * world / elapsed / 1e9, 1),
-        "config": {"workload": args.workload, "note": note, "M": M, "N": N, "K": K,
-                   "bits": bits, "group_size": group, "ring": R, "sz_bytes_per_group": 2 + zb,
-                   "graph": use_graph, "parallelism": f"weak x{world} (independent rings)"},
+        "config": {"workload": args.workload, "note": note, "M": M, "N": N_full, "K": K,
+                   "N_per_rank": N, "bits": bits, "group_size": group, "ring": R,
+                   "sz_bytes_per_group": 2 + zb, "graph": use_graph,
+                   "parallelism": (f"strong x{world} (output rows split, no collective)"
+                                   if args.split else f"weak x{world} (independent rings)")},
         "roofline": roof,
         "wall_s": round(wall, 4),
     }
