@@ -142,6 +142,25 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
                     int group, void* stream);
 
 /*
+ * The packed linear with a fused output epilogue (the decoder layer's glue around two of its
+ * linears, models/int_llama_layer.py of the reference):
+ *   QLIN_EP_RESIDUAL  y = RN16(residual + RN16(x @ W_dq^T + bias)) — o_proj / down_proj followed
+ *                     by `hidden_states = residual + hidden_states` (:241-257); residual [M, N].
+ *   QLIN_EP_SILU_MUL  W's rows interleaved in 8-row halves (rows 16j..16j+7 = gate rows
+ *                     8j..8j+7, rows 16j+8..16j+15 = up rows 8j..8j+7; N % 16 == 0):
+ *                     y[M, N/2] = RN16(RN16(silu(gate)) * up) with gate / up the fp16 F.linear
+ *                     outputs — QuantLlamaMLP's act_fn(gate_proj(x)) * up_proj(x) (:44-45).
+ *   QLIN_EP_NONE      == qlin_linear_f16.
+ * Same kernels and dispatch as qlin_linear_f16 (GEMV for M <= 64, MFMA GEMM above).
+ */
+#define QLIN_EP_NONE     0
+#define QLIN_EP_RESIDUAL 1
+#define QLIN_EP_SILU_MUL 2
+int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
+                       const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M,
+                       int64_t N, int64_t K, int bits, int group, int epilogue, void* stream);
+
+/*
  * Fused decode attention (one query token per sequence), for the quantized LLaMA layer's
  * attention core (models/int_llama_layer.py:137-165 of the reference: repeat_kv, fp32 QK^T bmm,
  * / sqrt(head_dim), + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV bmm) on an fp16 K/V

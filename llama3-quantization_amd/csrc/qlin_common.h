@@ -285,6 +285,27 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// output epilogues of the packed linear (qlin_linear_ep_f16); the accumulator (+ bias) is first
+// rounded to fp16 exactly as F.linear's output, then
+//   kEpResidual  y = RN16(residual + that)           (the decoder layer's `residual + h`)
+//   kEpSiluMul   rows interleaved in 8-row halves (gate rows 8j..8j+7 at tile rows 0-7, up rows
+//                at 8-15 of output tile j): y[:, 8j + n] = RN16(RN16(silu(gate)) * up), N/2 cols
+//                (QuantLlamaMLP's act_fn(gate_proj(x)) * up_proj(x))
+constexpr int kEpNone = 0;
+constexpr int kEpResidual = 1;
+constexpr int kEpSiluMul = 2;
+
+// the GEMV kernel with an output epilogue (qlin_gemv.hip), for qlin_linear_ep_f16
+int gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
+            const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
+            int64_t K, int bits, int group, int epilogue, void* stream);
+
+// torch's fp32 silu (x / (1 + exp(-x))) on an fp16 value, rounded to fp16
+__device__ __forceinline__ float silu_rn16(float g) {
+#pragma clang fp contract(off)
+  return (float)(_Float16)(g / (1.0f + expf(-g)));
+}
+
 }  // namespace qlin
 
 // zero mode from the layout flags (QLIN_FLOAT_ZERO wins: an fp16 zero is never "wide")

@@ -64,6 +64,11 @@ __device__ __forceinline__ void glds4(const void* g, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds((gbl_ptr)g, (lds_ptr)lds, 4, 0, 0);
 }
 
+struct GemmEp {  // output epilogue (qlin_common.h kEp*)
+  const uint16_t* res;
+  int ep;
+};
+
 struct GemmGeo {
   int64_t M;
   int N, K, Kt, G, group, wave, lane;
@@ -205,7 +210,8 @@ template <int BITS, bool WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW =
 __global__ __launch_bounds__(64 * NW) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
-    int64_t M, int N, int K, int group, uint32_t gmagic, int tiles_m, int tiles_n) {
+    int64_t M, int N, int K, int group, uint32_t gmagic, int tiles_m, int tiles_n,
+    const _Float16* __restrict__ res, int ep) {
   using C = Cfg<BITS, WN_, NW>;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * C::STAGE];
   GemmGeo g;
@@ -249,6 +255,27 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
   // epilogue: lane (n, q) holds C[4q + i][n] of each 16 x 16 block
   const int wm = g.wave / C::WGN, wn = g.wave % C::WGN;
   const int n_in = g.lane & 15, q = g.lane >> 4;
+  if (ep == kEpSiluMul) {  // N % 16 == 0: gate column n_in < 8 pairs with up column n_in + 8
+#pragma unroll
+    for (int nb = 0; nb < C::NB; ++nb) {
+      const int64_t j = g.nt0 + wn * C::NB + nb;  // interleaved tile = output columns 8j..8j+7
+      const int64_t n = j * kTileN + n_in;
+      const bool in_n = n < N;                    // wave-uniform
+      const float bv = (bias && in_n) ? (float)bias[n] : 0.f;
+#pragma unroll
+      for (int mb = 0; mb < C::MB; ++mb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float t = (float)(_Float16)(acc[mb][nb][i] + bv);
+          const float u = dpp_f<0x128>(t);  // row_ror:8 — lane n_in reads lane n_in + 8
+          const int64_t m = g.m0 + wm * C::WM + mb * 16 + 4 * q + i;
+          if (in_n && n_in < 8 && m < M)
+            y[m * (N >> 1) + j * 8 + n_in] = (_Float16)(silu_rn16(t) * u);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int nb = 0; nb < C::NB; ++nb) {
     const int64_t n = (g.nt0 + wn * C::NB + nb) * kTileN + n_in;
@@ -259,7 +286,11 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t m = g.m0 + wm * C::WM + mb * 16 + 4 * q + i;
-        if (m < M) y[m * N + n] = (_Float16)(acc[mb][nb][i] + bv);
+        if (m >= M) continue;
+        if (ep == kEpResidual)
+          y[m * N + n] = (_Float16)((float)(_Float16)(acc[mb][nb][i] + bv) + (float)res[m * N + n]);
+        else
+          y[m * N + n] = (_Float16)(acc[mb][nb][i] + bv);
       }
     }
   }
@@ -272,7 +303,7 @@ uint32_t group_magic(int group) {
 
 template <int BITS, bool WN_, int GPT, int ZM>
 int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                  uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
+                  uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
   const int tiles_n = (N + Cfg<BITS, WN_>::BN - 1) / Cfg<BITS, WN_>::BN;
   const int64_t tiles_m = (M + BM - 1) / BM;
   const int64_t blocks = tiles_m * tiles_n;
@@ -280,7 +311,8 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
 #define QLIN_GL(KF)                                                                           \
   hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, ZM, KF, 0, kWaves>), dim3((unsigned)blocks), \
                      dim3(64 * kWaves), 0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, \
-                     (_Float16*)y, M, N, K, group, group_magic(group), (int)tiles_m, tiles_n)
+                     (_Float16*)y, M, N, K, group, group_magic(group), (int)tiles_m, tiles_n, \
+                     (const _Float16*)e.res, e.ep)
   // straight-line k-steps need K % 128 == 0; the wide tile with 2-4 group slots per k-tile then
   // spills (the per-step checks bound the scheduler), so it keeps the checked form
   if (K % BK == 0 && !(WN_ && GPT > 1)) QLIN_GL(true);
@@ -293,21 +325,21 @@ constexpr int64_t kWideMinBlocks = 512;  // >= 2 blocks per CU on 256 CUs
 
 template <int BITS, int GPT, int ZM>
 int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
+                uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
   if constexpr (BITS != 8) {
     const int64_t wide_blocks = ((M + BM - 1) / BM) * ((N + 511) / 512);
     if (wide_blocks >= kWideMinBlocks)
-      return launch_gemm_t<BITS, true, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+      return launch_gemm_t<BITS, true, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   }
-  return launch_gemm_t<BITS, false, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+  return launch_gemm_t<BITS, false, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
 }
 
 template <int BITS, int ZM>
 int launch_gemm_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                  uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st) {
-  if (group % 128 == 0) return launch_gemm<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
-  if (group % 64 == 0) return launch_gemm<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
-  return launch_gemm<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+                  uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
+  if (group % 128 == 0) return launch_gemm<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+  if (group % 64 == 0) return launch_gemm<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+  return launch_gemm<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
 }
 
 bool valid(int64_t M, int64_t N, int64_t K, int bits, int group) {
@@ -318,20 +350,20 @@ bool valid(int64_t M, int64_t N, int64_t K, int bits, int group) {
 
 }  // namespace
 
-extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
-                             const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
-                             int64_t N, int64_t K, int bits, int group, void* workspace,
-                             void* stream) {
-  (void)workspace;
+namespace {
+int gemm_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
+            const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
+            int64_t K, int bits, int group, int epilogue, void* stream) {
   if (!qweight || !qsz || !x || !y || !valid(M, N, K, bits, group)) return QLIN_EINVAL;
   if (M == 0 || N == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
+  const GemmEp e{residual, epilogue};
   const int zm = zero_mode(flags);
   const int n = (int)N, k = (int)K;
 #define QLIN_M(B)                                                                              \
-  return zm == kZFloat  ? launch_gemm_g<B, kZFloat>(qweight, qsz, x, bias, y, M, n, k, group, st) \
-         : zm == kZWide ? launch_gemm_g<B, kZWide>(qweight, qsz, x, bias, y, M, n, k, group, st)  \
-                        : launch_gemm_g<B, kZNarrow>(qweight, qsz, x, bias, y, M, n, k, group, st)
+  return zm == kZFloat  ? launch_gemm_g<B, kZFloat>(qweight, qsz, x, bias, y, M, n, k, group, st, e) \
+         : zm == kZWide ? launch_gemm_g<B, kZWide>(qweight, qsz, x, bias, y, M, n, k, group, st, e)  \
+                        : launch_gemm_g<B, kZNarrow>(qweight, qsz, x, bias, y, M, n, k, group, st, e)
   switch (bits) {
     case 2: QLIN_M(2);
     case 3: QLIN_M(3);
@@ -339,6 +371,15 @@ extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int f
     default: QLIN_M(8);
   }
 #undef QLIN_M
+}
+}  // namespace
+
+extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                             const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
+                             int64_t N, int64_t K, int bits, int group, void* workspace,
+                             void* stream) {
+  (void)workspace;
+  return gemm_ep(qweight, qsz, flags, x, bias, nullptr, y, M, N, K, bits, group, kEpNone, stream);
 }
 
 extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
@@ -357,4 +398,28 @@ extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int
     return QLIN_OK;
   }
   return qlin_gemm_f16(qweight, qsz, flags, x, bias, y, M, N, K, bits, group, nullptr, stream);
+}
+
+extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                                  const uint16_t* x, const uint16_t* bias,
+                                  const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
+                                  int64_t K, int bits, int group, int epilogue, void* stream) {
+  if (epilogue < kEpNone || epilogue > kEpSiluMul) return QLIN_EINVAL;
+  if (epilogue == kEpResidual && !residual) return QLIN_EINVAL;
+  if (epilogue == kEpSiluMul && N % kTileN) return QLIN_EINVAL;
+  if (M < 0) return QLIN_EINVAL;
+  if (M == 0) return QLIN_OK;
+  const int64_t ny = epilogue == kEpSiluMul ? N / 2 : N;  // columns of y (and residual)
+  if (M <= kSkinnyMaxM) {
+    for (int64_t m0 = 0; m0 < M; m0 += 16) {
+      const int64_t mc = M - m0 < 16 ? M - m0 : 16;
+      const int rc = qlin::gemv_ep(qweight, qsz, flags, x + m0 * K, bias,
+                                   residual ? residual + m0 * ny : nullptr, y + m0 * ny, mc, N, K,
+                                   bits, group, epilogue, stream);
+      if (rc) return rc;
+    }
+    return QLIN_OK;
+  }
+  return gemm_ep(qweight, qsz, flags, x, bias, residual, y, M, N, K, bits, group, epilogue,
+                 stream);
 }

@@ -37,6 +37,11 @@ using namespace qlin;
 namespace {
 
 constexpr int kMaxWaves = 16;
+
+struct Ep {  // output epilogue (qlin_common.h kEp*)
+  const uint16_t* res;
+  int ep;
+};
 constexpr int kGemvMaxM = 16;  // one MFMA row block
 
 template <int BITS, int GPT>
@@ -179,7 +184,8 @@ template <int BITS, int MT, int GPT, int ZM, int PF>
 __global__ __launch_bounds__(1024) void gemv_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
-    int M, int N, int K, int group, uint32_t gmagic, int tpw) {
+    int M, int N, int K, int group, uint32_t gmagic, int tpw, const _Float16* __restrict__ res,
+    int ep) {
   __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
   const int W = blockDim.x >> 6;
@@ -223,15 +229,31 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
   }
   __syncthreads();
   // MT * 16 outputs; a block of W < MT / 4 waves (short K) loops
-  for (int o = tid; o < MT * kTileN; o += blockDim.x) {
-    const int m = o / kTileN, n = o - m * kTileN;
-    const int64_t row = (int64_t)nt * kTileN + n;
+  auto total = [&](int o, int64_t row) {
     const f4* r = reinterpret_cast<const f4*>(red + o * kMaxWaves);
     const f4 a = r[0], b = r[1], c = r[2], d = r[3];
     const f4 e = (a + b) + (c + d);
     float t = (e[0] + e[1]) + (e[2] + e[3]);
+    if (bias) t += (float)bias[row];
+    return (float)(_Float16)t;  // F.linear's fp16 output
+  };
+  if (ep == kEpSiluMul) {  // N even, interleaved halves: 8 outputs per tile and row m
+    for (int o = tid; o < MT * 8; o += blockDim.x) {
+      const int m = o >> 3, n = o & 7;
+      const int64_t row = (int64_t)nt * kTileN + n;
+      if (m < M && row + 8 < N) {
+        const float g = total(m * kTileN + n, row), u = total(m * kTileN + n + 8, row + 8);
+        y[(int64_t)m * (N >> 1) + nt * 8 + n] = (_Float16)(silu_rn16(g) * u);
+      }
+    }
+    return;
+  }
+  for (int o = tid; o < MT * kTileN; o += blockDim.x) {
+    const int m = o / kTileN, n = o - m * kTileN;
+    const int64_t row = (int64_t)nt * kTileN + n;
     if (m < M && row < N) {
-      if (bias) t += (float)bias[row];
+      float t = total(o, row);
+      if (ep == kEpResidual) t += (float)res[(int64_t)m * N + row];
       y[(int64_t)m * N + row] = (_Float16)t;
     }
   }
@@ -292,7 +314,7 @@ int pick_waves(int Nt, int Kt, int& tpw) {
 
 template <int BITS, int MT, int GPT, int ZM>
 int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                  uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
+                  uint16_t* y, int M, int N, int K, int group, hipStream_t st, const Ep& e) {
   const int Nt = (N + kTileN - 1) / kTileN;
   const int Kt = (K + kTileK - 1) / kTileK;
   int tpw = 0;
@@ -301,7 +323,7 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
 #define QLIN_GV(PF)                                                                        \
   hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, ZM, PF>), dim3(Nt), dim3(64 * W), \
                      0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias,             \
-                     (_Float16*)y, M, N, K, group, gs, tpw)
+                     (_Float16*)y, M, N, K, group, gs, tpw, (const _Float16*)e.res, e.ep)
   if constexpr (MT >= 8) {  // x registers of 4 tiles in flight would spill
     QLIN_GV(2);
   } else {
@@ -314,22 +336,22 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
 
 template <int BITS, int MT, int ZM>
 int launch_gemv_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                  uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
+                  uint16_t* y, int M, int N, int K, int group, hipStream_t st, const Ep& e) {
   if (group % 128 == 0)
-    return launch_gemv<BITS, MT, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+    return launch_gemv<BITS, MT, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   if (group % 64 == 0)
-    return launch_gemv<BITS, MT, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
-  return launch_gemv<BITS, MT, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+    return launch_gemv<BITS, MT, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+  return launch_gemv<BITS, MT, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
 }
 
 template <int BITS, int ZM>
 int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                  uint16_t* y, int M, int N, int K, int group, hipStream_t st) {
-  if (M == 1) return launch_gemv_g<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
-  if (M == 2) return launch_gemv_g<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
-  if (M <= 4) return launch_gemv_g<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
-  if (M <= 8) return launch_gemv_g<BITS, 8, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
-  return launch_gemv_g<BITS, 16, ZM>(qw, qsz, x, bias, y, M, N, K, group, st);
+                  uint16_t* y, int M, int N, int K, int group, hipStream_t st, const Ep& e) {
+  if (M == 1) return launch_gemv_g<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+  if (M == 2) return launch_gemv_g<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+  if (M <= 4) return launch_gemv_g<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+  if (M <= 8) return launch_gemv_g<BITS, 8, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+  return launch_gemv_g<BITS, 16, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
 }
 
 }  // namespace
@@ -361,19 +383,22 @@ extern "C" int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, in
   return (int)hipGetLastError();
 }
 
-extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
-                             const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
-                             int64_t N, int64_t K, int bits, int group, void* stream) {
+// GEMV with an output epilogue (qlin_linear_ep_f16's M <= 16 leg)
+int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                                     const uint16_t* x, const uint16_t* bias,
+                                     const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
+                                     int64_t K, int bits, int group, int epilogue, void* stream) {
   if (!qweight || !qsz || !x || !y || M < 1 || M > kGemvMaxM || !valid_layout(N, K, bits, group))
     return QLIN_EINVAL;
   if (N == 0) return QLIN_OK;
+  const Ep e{residual, epilogue};
   hipStream_t st = (hipStream_t)stream;
   const int m = (int)M, n = (int)N, k = (int)K;
   const int zm = zero_mode(flags);
 #define QLIN_G(B)                                                                           \
-  return zm == kZFloat  ? launch_gemv_m<B, kZFloat>(qweight, qsz, x, bias, y, m, n, k, group, st) \
-         : zm == kZWide ? launch_gemv_m<B, kZWide>(qweight, qsz, x, bias, y, m, n, k, group, st)  \
-                        : launch_gemv_m<B, kZNarrow>(qweight, qsz, x, bias, y, m, n, k, group, st)
+  return zm == kZFloat  ? launch_gemv_m<B, kZFloat>(qweight, qsz, x, bias, y, m, n, k, group, st, e) \
+         : zm == kZWide ? launch_gemv_m<B, kZWide>(qweight, qsz, x, bias, y, m, n, k, group, st, e)  \
+                        : launch_gemv_m<B, kZNarrow>(qweight, qsz, x, bias, y, m, n, k, group, st, e)
   switch (bits) {
     case 2: QLIN_G(2);
     case 3: QLIN_G(3);
@@ -381,4 +406,11 @@ extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int f
     default: QLIN_G(8);
   }
 #undef QLIN_G
+}
+
+extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                             const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
+                             int64_t N, int64_t K, int bits, int group, void* stream) {
+  return qlin::gemv_ep(qweight, qsz, flags, x, bias, nullptr, y, M, N, K, bits, group,
+                               kEpNone, stream);
 }

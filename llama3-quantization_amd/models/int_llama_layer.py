@@ -19,7 +19,8 @@ import torch
 from torch import nn
 
 from quant import qlin
-from quant.int_linear import FusedPackedLinear, QuantLinear
+from quant.int_linear import (FusedPackedLinear, QuantLinear, SiluMulPackedLinear,
+                              packed_residual_linear)
 from quant.int_matmul import QuantMatMul
 from quant.omni_norm import OmniLlamaRMSNorm
 
@@ -96,18 +97,37 @@ class QuantLlamaMLP(nn.Module):
         self.down_proj = QuantLinear(org_module.down_proj, args.weight_quant_params, args.act_quant_params)
         self.up_proj = QuantLinear(org_module.up_proj, args.weight_quant_params, args.act_quant_params)
         self.act_fn = _act(hidden_act)
+        self.hidden_act = hidden_act
         self.gate_up = None  # FusedPackedLinear after fuse_packed()
+        self.gate_up_act = None  # SiluMulPackedLinear after fuse_packed() (SiLU models)
 
     def fuse_packed(self):
-        """gate_proj + up_proj as one fused packed launch (both read x)."""
-        self.gate_up = FusedPackedLinear([self.gate_proj, self.up_proj])
+        """gate_proj + up_proj as one fused packed launch (both read x); with SiLU the activation
+        product is applied in that launch's epilogue."""
+        if self.hidden_act == "silu" and self.gate_proj.out_features % 16 == 0:
+            self.gate_up_act = SiluMulPackedLinear(self.gate_proj, self.up_proj)
+        else:
+            self.gate_up = FusedPackedLinear([self.gate_proj, self.up_proj])
         return self
 
-    def forward(self, x):
-        if self.gate_up is not None and not self.gate_proj.use_act_quant:
-            gate, up = self.gate_up(x)
-            return self.down_proj(self.act_fn(gate) * up)
-        return self.down_proj(self.act_fn(self.gate_proj(x)) * self.up_proj(x))
+    def fused(self):
+        return (self.gate_up is not None or self.gate_up_act is not None) and \
+            not self.gate_proj.use_act_quant
+
+    def forward(self, x, residual=None):
+        """``down(act(gate(x)) * up(x))``; with ``residual`` (fused packed mode only) the
+        decoder layer's ``residual + mlp(x)`` is folded into down_proj's epilogue."""
+        if self.fused():
+            if self.gate_up_act is not None:
+                h = self.gate_up_act(x)
+            else:
+                gate, up = self.gate_up(x)
+                h = self.act_fn(gate) * up
+            if residual is not None:
+                return packed_residual_linear(self.down_proj, h, residual)
+            return self.down_proj(h)
+        out = self.down_proj(self.act_fn(self.gate_proj(x)) * self.up_proj(x))
+        return out if residual is None else residual + out
 
 
 class QuantLlamaAttention(nn.Module):
@@ -163,6 +183,13 @@ class QuantLlamaAttention(nn.Module):
             return self.qkv(hidden_states)
         return self.q_proj(hidden_states), self.k_proj(hidden_states), self.v_proj(hidden_states)
 
+    def _out(self, attn_output, residual):
+        if residual is None:
+            return self.o_proj(attn_output)
+        if self.o_proj.packed and not self.o_proj.use_act_quant:
+            return packed_residual_linear(self.o_proj, attn_output, residual)
+        return residual + self.o_proj(attn_output)
+
     def _shape(self, tensor: torch.Tensor, seq_len: int, bsz: int):
         return tensor.view(bsz, seq_len, self.num_heads, self.head_dim).transpose(1, 2).contiguous()
 
@@ -174,7 +201,10 @@ class QuantLlamaAttention(nn.Module):
         past_key_value: Optional[Tuple[torch.Tensor]] = None,
         output_attentions: bool = False,
         use_cache: bool = False,
+        residual: Optional[torch.Tensor] = None,
     ):
+        """``residual`` (fused packed mode, set by the decoder layer): the output is
+        ``residual + o_proj(attn)``, the add folded into o_proj's epilogue."""
         bsz, q_len, _ = hidden_states.size()
         act_dtype = hidden_states.dtype
         q, k, v = self._project(hidden_states)
@@ -202,7 +232,7 @@ class QuantLlamaAttention(nn.Module):
             attn_output = qlin.attn_decode(query_states, key_states, value_states, attention_mask,
                                            math.sqrt(self.head_dim))
             attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
-            return self.o_proj(attn_output), None, past_key_value
+            return self._out(attn_output, residual), None, past_key_value
 
         key_states = repeat_kv(key_states, self.num_key_value_groups)
         value_states = repeat_kv(value_states, self.num_key_value_groups)
@@ -234,7 +264,7 @@ class QuantLlamaAttention(nn.Module):
                 f"`attn_output` should be of size {(bsz, self.num_heads, q_len, self.head_dim)}, but is"
                 f" {attn_output.size()}")
         attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
-        attn_output = self.o_proj(attn_output)
+        attn_output = self._out(attn_output, residual)
         if not output_attentions:
             attn_weights = None
         return attn_output, attn_weights, past_key_value
@@ -258,6 +288,7 @@ class QuantLlamaDecoderLayer(nn.Module):
         self.input_layernorm = OmniLlamaRMSNorm(ori_layer.input_layernorm, eps=ori_layer.input_layernorm.variance_epsilon)
         self.post_attention_layernorm = OmniLlamaRMSNorm(ori_layer.post_attention_layernorm, eps=ori_layer.post_attention_layernorm.variance_epsilon)
         self.let = False
+        self.fused_epilogues = False  # fuse_packed_projections() turns it on
 
     def forward(
         self,
@@ -270,14 +301,25 @@ class QuantLlamaDecoderLayer(nn.Module):
     ):
         residual = hidden_states
         hidden_states = self.input_layernorm(hidden_states)
-        hidden_states, self_attn_weights, present_key_value = self.self_attn(
-            hidden_states=hidden_states, attention_mask=attention_mask, position_ids=position_ids,
-            past_key_value=past_key_value, output_attentions=output_attentions, use_cache=use_cache)
-        hidden_states = residual + hidden_states
-        residual = hidden_states
-        hidden_states = self.post_attention_layernorm(hidden_states)
-        hidden_states = self.mlp(hidden_states)
-        hidden_states = residual + hidden_states
+        if self.fused_epilogues and self.mlp.fused():
+            # fused packed mode: both residual adds run in the o_proj / down_proj epilogues
+            # (same fp16 arithmetic: RN16(residual + RN16(linear)))
+            hidden_states, self_attn_weights, present_key_value = self.self_attn(
+                hidden_states=hidden_states, attention_mask=attention_mask,
+                position_ids=position_ids, past_key_value=past_key_value,
+                output_attentions=output_attentions, use_cache=use_cache, residual=residual)
+            residual = hidden_states
+            hidden_states = self.mlp(self.post_attention_layernorm(hidden_states), residual=residual)
+        else:
+            hidden_states, self_attn_weights, present_key_value = self.self_attn(
+                hidden_states=hidden_states, attention_mask=attention_mask,
+                position_ids=position_ids, past_key_value=past_key_value,
+                output_attentions=output_attentions, use_cache=use_cache)
+            hidden_states = residual + hidden_states
+            residual = hidden_states
+            hidden_states = self.post_attention_layernorm(hidden_states)
+            hidden_states = self.mlp(hidden_states)
+            hidden_states = residual + hidden_states
         outputs = (hidden_states,)
         if output_attentions:
             outputs += (self_attn_weights,)
@@ -293,9 +335,11 @@ class QuantLlamaDecoderLayer(nn.Module):
                 m.set_quant_state(weight_quant, act_quant)
 
     def fuse_packed_projections(self):
-        """After packing: q/k/v and gate/up each become one fused launch."""
+        """After packing: q/k/v and gate/up (+ SiLU·mul) each become one fused launch, and the two
+        residual adds move into the o_proj / down_proj epilogues."""
         self.self_attn.fuse_packed()
         self.mlp.fuse_packed()
+        self.fused_epilogues = self.self_attn.o_proj.packed and self.mlp.down_proj.packed
         return self
 
     @torch.no_grad()

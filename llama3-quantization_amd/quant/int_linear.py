@@ -206,3 +206,54 @@ class FusedPackedLinear(nn.Module):
         if x.dtype != torch.float16:
             y = y.to(x.dtype)
         return torch.split(y, self.splits, dim=-1)
+
+
+class SiluMulPackedLinear(nn.Module):
+    """gate_proj + up_proj + ``act_fn(gate) * up`` (QuantLlamaMLP, SiLU) as ONE packed launch: the
+    two matrices' rows interleaved in 8-row halves (``qlin.interleave_gate_up``) and the SiLU·mul
+    applied in the kernel epilogue (``QLIN_EP_SILU_MUL``) on the fp16 gate / up values, so the
+    [M, 2I] gate/up tensor is never written.  Same per-element arithmetic as the unfused modules
+    (the dequant-matmul accumulators are identical; silu is fp32 x / (1 + exp(-x)) rounded to
+    fp16 as torch's)."""
+
+    def __init__(self, gate, up):
+        super().__init__()
+        if not (gate.packed and up.packed):
+            raise ValueError("SiluMulPackedLinear needs packed QuantLinear members")
+        if (gate.in_features, gate.out_features, gate.wbits, gate.group) != \
+                (up.in_features, up.out_features, up.wbits, up.group):
+            raise ValueError("gate and up must have the same shape, bits and group")
+        if gate.out_features % qlin.TILE_N:
+            raise ValueError("gate/up out_features must be a multiple of 16")
+        self.in_features = gate.in_features
+        self.out_features = gate.out_features  # of the product silu(gate) * up
+        self.wbits, self.group = gate.wbits, gate.group
+        qw, qsz = qlin.interleave_gate_up(gate.qweight, gate.qsz, up.qweight, up.qsz)
+        self.register_buffer("qweight", qw)
+        self.register_buffer("qsz", qsz)
+        self.qflags = gate.qflags | up.qflags
+        if gate.bias is not None or up.bias is not None:
+            I, dev = self.out_features, qw.device
+            z = torch.zeros(I, dtype=torch.float16, device=dev)
+            gb = gate.bias.to(torch.float16) if gate.bias is not None else z
+            ub = up.bias.to(torch.float16) if up.bias is not None else z
+            self.register_buffer("bias", torch.stack([gb.view(-1, 8), ub.view(-1, 8)], 1).reshape(-1))
+        else:
+            self.bias = None
+
+    def forward(self, x):
+        xin = x if x.dtype == torch.float16 else x.to(torch.float16)
+        y = qlin.linear_ep(xin.contiguous(), self.qweight, self.qsz, self.bias,
+                           2 * self.out_features, self.in_features, self.wbits, self.group,
+                           self.qflags, epilogue=qlin.EP_SILU_MUL)
+        return y if x.dtype == torch.float16 else y.to(x.dtype)
+
+
+def packed_residual_linear(lin, x, residual):
+    """``residual + lin(x)`` for a packed QuantLinear as one launch (``QLIN_EP_RESIDUAL``): the
+    decoder layer's residual add fused into o_proj / down_proj's output."""
+    xin = x if x.dtype == torch.float16 else x.to(torch.float16)
+    bias = None if lin.bias is None else lin.bias.to(torch.float16).contiguous()
+    return qlin.linear_ep(xin.contiguous(), lin.qweight, lin.qsz, bias, lin.out_features,
+                          lin.in_features, lin.wbits, lin.group, lin.qflags,
+                          epilogue=qlin.EP_RESIDUAL, residual=residual.contiguous())

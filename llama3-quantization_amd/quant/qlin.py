@@ -46,6 +46,7 @@ SIGNATURES = {
     "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
+    "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _p], _i),
     "qlin_attn_decode_partials_bytes": ([_l, _i, _i, _l], _l),
     "qlin_attn_decode": ([_p, _p, _p, _p, _p, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p], _i),
 }
@@ -290,6 +291,57 @@ def gemv(x, qweight, qsz, bias, N, K, bits, group, flags=0):
 def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0):
     return _linear_call("qlin_gemm_f16", x, qweight, qsz, bias, N, K, bits, group, flags,
                         extra=(None,))
+
+
+EP_NONE = 0
+EP_RESIDUAL = 1
+EP_SILU_MUL = 2
+
+
+def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NONE,
+              residual=None):
+    """``qlin_linear_ep_f16``: the packed linear with a fused output epilogue.
+
+    EP_RESIDUAL: ``residual + F.linear(x)`` (residual fp16, shape of the output).
+    EP_SILU_MUL: rows interleaved by ``interleave_gate_up``; returns ``silu(gate) * up`` with
+    N / 2 columns."""
+    _dev(x, qweight, qsz, bias, residual)
+    if x.dtype != torch.float16:
+        raise ValueError(f"packed linear takes fp16 activations, got {x.dtype}")
+    if x.shape[-1] != K:
+        raise ValueError(f"input has {x.shape[-1]} features, layer expects {K}")
+    if bias is not None and (bias.dtype != torch.float16 or bias.numel() != N):
+        raise ValueError("bias must be fp16 [N]")
+    _check_packed(qweight, qsz, N, K, bits, group)
+    ny = N // 2 if epilogue == EP_SILU_MUL else N
+    y = torch.empty(*x.shape[:-1], ny, dtype=torch.float16, device=x.device)
+    if epilogue == EP_RESIDUAL:
+        if residual is None or residual.dtype != torch.float16 or residual.shape != y.shape:
+            raise ValueError(f"residual must be fp16 {tuple(y.shape)}")
+    M = x.numel() // K if K else 0
+    if M == 0:
+        return y
+    rc = load_library().qlin_linear_ep_f16(_ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(bias),
+                                           _ptr(residual), _ptr(y), M, N, K, bits, group,
+                                           epilogue, _stream(x))
+    _check(rc, "qlin_linear_ep_f16")
+    return y
+
+
+def interleave_gate_up(qw_gate, qsz_gate, qw_up, qsz_up):
+    """Packed gate / up matrices (same N, a multiple of 16) -> one matrix whose 16-row tile j
+    holds gate rows 8j..8j+7 then up rows 8j..8j+7 (the EP_SILU_MUL row order).  A permutation
+    of whole lane pieces and (scale, zero) words: no value changes."""
+    T, Kt, _, b = qw_gate.shape
+    G = qsz_gate.shape[1]
+    if qw_up.shape != qw_gate.shape or qsz_up.shape != qsz_gate.shape:
+        raise ValueError("gate and up must have the same packed shapes")
+    # qweight [T, Kt, 64 = 4 q x 16 n, b] -> [T, half, Kt, q, 8, b]
+    pw = lambda w: w.view(T, Kt, 4, 2, 8, b).permute(0, 3, 1, 2, 4, 5)
+    qw = torch.stack([pw(qw_gate), pw(qw_up)], dim=4).reshape(2 * T, Kt, 64, b)
+    ps = lambda z: z.view(T, G, 2, 8).permute(0, 2, 1, 3)
+    qsz = torch.stack([ps(qsz_gate), ps(qsz_up)], dim=3).reshape(2 * T, G, 16)
+    return qw.contiguous(), qsz.contiguous()
 
 
 ATTN_MAX_L = 4096

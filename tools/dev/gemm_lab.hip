@@ -12,7 +12,7 @@ extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
 #define L(W, A, NW)                                                                             \
   hipLaunchKernelGGL((gemm_kernel<4, W, 1, kZNarrow, true, A, NW>), grid, dim3(64 * NW), 0,     \
                      (hipStream_t)stream, qw, qsz, (const _Float16*)x, nullptr, (_Float16*)y, M, \
-                     N, K, 128, group_magic(128), tiles_m, tiles_n)
+                     N, K, 128, group_magic(128), tiles_m, tiles_n, nullptr, 0)
 #define LA(W, NW) \
   { if (a == 0) L(W, 0, NW); else if (a == 1) L(W, 1, NW); else if (a == 2) L(W, 2, NW); else L(W, 3, NW); }
   const int a = abl & 3;
