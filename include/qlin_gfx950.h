@@ -179,6 +179,32 @@ int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const
                      float* out, int64_t B, int Hq, int Hkv, int64_t L, int D, float scale_div,
                      float* partials, int32_t* counters, void* stream);
 
+/*
+ * RMSNorm of the quantized LLaMA layer (OmniLlamaRMSNorm.forward, quant/omni_norm.py:52-63 of the
+ * reference): y = (weight * (x * rsqrt(mean(x^2) + eps))).to(fp16), fp32 inside.
+ *   x, y  fp16 [rows, H];  weight  fp32 [H] (the fp16 weight upcast: exact).
+ * The sum of squares runs in another order than torch's reduction: y may differ by one fp16 ulp.
+ */
+int qlin_rmsnorm_f16(const uint16_t* x, const float* weight, uint16_t* y, int64_t rows, int64_t H,
+                     float eps, void* stream);
+
+/*
+ * Rotary position embedding of QuantLlamaAttention.forward (models/int_llama_layer.py:116-125 of
+ * the reference, transformers-4.37.2 apply_rotary_pos_emb): bit-exact, in one launch.
+ *   q  fp16 rows of Hq*D, row (b, s) at q + (b*S + s)*q_row_stride (e.g. a column slice of the
+ *      fused q/k/v output);  k  likewise with Hkv heads;
+ *   cos_cache, sin_cache  fp32 [cache_rows, D] (the rotary cache; each value is cast to fp16 as
+ *      the reference's rotary_emb(...).to(x.dtype) does); positions outside [0, cache_rows) are
+ *      clamped (the reference's index raises instead);
+ *   position_ids  int64, (b, s) at position_ids[b*pos_batch_stride + s];
+ *   q_out  fp32 [B, Hq, S, D]: q.transpose(1, 2).float() * cos + rotate_half(.) * sin (fp32 ops);
+ *   k_out  fp16 [B, Hkv, S, D]: the same in fp16 ops (each product and the sum rounded to fp16).
+ */
+int qlin_rope_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k, int64_t k_row_stride,
+                  const float* cos_cache, const float* sin_cache, int64_t cache_rows,
+                  const int64_t* position_ids, int64_t pos_batch_stride, float* q_out, uint16_t* k_out, int64_t B, int64_t S,
+                  int Hq, int Hkv, int D, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,118 @@
+// qlin_layer.hip — the decoder layer's elementwise glue around the quantized linears, gfx950:
+// RMSNorm and rotary position embedding, one launch each (the reference runs each as 5-14
+// PyTorch kernels per layer and token; at batch-1 decode they cost more than the 7 packed
+// linears' HBM time).
+//
+// qlin_rmsnorm_f16 replaces OmniLlamaRMSNorm.forward (quant/omni_norm.py:52-63 of the reference):
+//   var = mean(x.float()^2); h = x * rsqrt(var + eps) (fp32); y = (weight * h).to(fp16).
+// One block per row; the sum of squares runs in a different order than torch's reduction, so y
+// can differ from the reference by one fp16 ulp where var's last bit differs.
+//
+// qlin_rope_f16 replaces, in QuantLlamaAttention.forward (models/int_llama_layer.py:116-125),
+// the q/k reshape + transpose, q's cast to fp32, rotary_emb(cos/sin cache slice, cast to fp16)
+// and apply_rotary_pos_emb (index by position_ids, q*cos + rotate_half(q)*sin in fp32 for q,
+// the same in fp16 for k: every product and the sum rounded to fp16 as torch's fp16 ops do).
+// Elementwise with the reference's op order and roundings: bit-exact.
+#include "qlin_common.h"
+#include "../../include/qlin_gfx950.h"
+
+namespace {
+
+constexpr int kNormThreads = 256;
+
+__global__ __launch_bounds__(kNormThreads) void rmsnorm_kernel(
+    const _Float16* __restrict__ x, const float* __restrict__ w, _Float16* __restrict__ y,
+    int64_t H, float eps) {
+#pragma clang fp contract(off)
+  __shared__ float part[kNormThreads / 64];
+  const int64_t row = blockIdx.x;
+  const _Float16* xr = x + row * H;
+  float ss = 0.f;
+  for (int64_t i = threadIdx.x; i < H; i += kNormThreads) {
+    const float v = (float)xr[i];
+    ss += v * v;
+  }
+  // wave sum (rows of 16, then the four row totals), then the block's waves
+  ss = qlin::row16_sum(ss);
+  ss += __shfl_xor(ss, 16);
+  ss += __shfl_xor(ss, 32);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int i = 0; i < kNormThreads / 64; ++i) tot += part[i];
+  const float var = tot / (float)H;
+  const float r = rsqrtf(var + eps);
+  _Float16* yr = y + row * H;
+  for (int64_t i = threadIdx.x; i < H; i += kNormThreads) {
+    const float h = (float)xr[i] * r;
+    yr[i] = (_Float16)(w[i] * h);
+  }
+}
+
+// one thread per (b, s, head, d) of q (Hq heads) and k (Hkv heads)
+__global__ __launch_bounds__(256) void rope_kernel(
+    const _Float16* __restrict__ q, int64_t q_rs, const _Float16* __restrict__ k, int64_t k_rs,
+    const float* __restrict__ cosc, const float* __restrict__ sinc, int64_t cache_rows,
+    const int64_t* __restrict__ pos, int64_t pos_bs, float* __restrict__ q_out,
+    _Float16* __restrict__ k_out, int64_t B, int64_t S, int Hq, int Hkv, int D) {
+#pragma clang fp contract(off)
+  const int64_t total = B * S * (int64_t)(Hq + Hkv) * D;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int d = (int)(i % D);
+  int64_t t = i / D;
+  const int h = (int)(t % (Hq + Hkv));
+  t /= (Hq + Hkv);
+  const int64_t s = t % S, b = t / S;
+  // positions outside the cache are clamped (never read out of bounds; the reference raises)
+  const int64_t p = min(max(pos[b * pos_bs + s], (int64_t)0), cache_rows - 1);
+  // the reference's cos/sin: the fp32 cache sliced and cast to the activation dtype (fp16)
+  const float c = (float)(_Float16)cosc[p * D + d];
+  const float sn = (float)(_Float16)sinc[p * D + d];
+  const int half = D / 2;
+  const int dr = d < half ? d + half : d - half;  // rotate_half partner
+  if (h < Hq) {
+    const _Float16* qr = q + (b * S + s) * q_rs + (int64_t)h * D;
+    const float v = (float)qr[d];
+    const float rv = d < half ? -(float)qr[dr] : (float)qr[dr];
+    q_out[((b * Hq + h) * S + s) * D + d] = v * c + rv * sn;  // fp32, each op rounded once
+  } else {
+    const int hk = h - Hq;
+    const _Float16* kr = k + (b * S + s) * k_rs + (int64_t)hk * D;
+    const float v = (float)kr[d];
+    const float rv = d < half ? -(float)kr[dr] : (float)kr[dr];
+    const float a = (float)(_Float16)(v * c), bb = (float)(_Float16)(rv * sn);
+    k_out[((b * Hkv + hk) * S + s) * D + d] = (_Float16)(a + bb);
+  }
+}
+
+}  // namespace
+
+extern "C" int qlin_rmsnorm_f16(const uint16_t* x, const float* weight, uint16_t* y, int64_t rows,
+                                int64_t H, float eps, void* stream) {
+  if (!x || !weight || !y || rows < 0 || H <= 0 || rows > 0x7fffffff) return QLIN_EINVAL;
+  if (rows == 0) return QLIN_OK;
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3((unsigned)rows), dim3(kNormThreads), 0,
+                     (hipStream_t)stream, (const _Float16*)x, weight, (_Float16*)y, H, eps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qlin_rope_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+                             int64_t k_row_stride, const float* cos_cache, const float* sin_cache,
+                             int64_t cache_rows, const int64_t* position_ids,
+                             int64_t pos_batch_stride, float* q_out, uint16_t* k_out, int64_t B,
+                             int64_t S, int Hq, int Hkv, int D, void* stream) {
+  if (!q || !k || !cos_cache || !sin_cache || !position_ids || !q_out || !k_out || B < 0 ||
+      S < 0 || Hq <= 0 || Hkv <= 0 || D <= 0 || D % 2 || q_row_stride < (int64_t)Hq * D ||
+      k_row_stride < (int64_t)Hkv * D || pos_batch_stride < 0 || cache_rows <= 0)
+    return QLIN_EINVAL;
+  const int64_t total = B * S * (int64_t)(Hq + Hkv) * D;
+  if (total == 0) return QLIN_OK;
+  if ((total + 255) / 256 > 0x7fffffff) return QLIN_EINVAL;
+  hipLaunchKernelGGL(rope_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const _Float16*)q, q_row_stride, (const _Float16*)k,
+                     k_row_stride, cos_cache, sin_cache, cache_rows, position_ids,
+                     pos_batch_stride, q_out, (_Float16*)k_out, B, S, Hq, Hkv, D);
+  return (int)hipGetLastError();
+}

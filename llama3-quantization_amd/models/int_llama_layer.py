@@ -163,12 +163,14 @@ class QuantLlamaAttention(nn.Module):
         self.use_act_quant = False
         self.qkv = None  # FusedPackedLinear after fuse_packed()
         self.decode_kernel = False  # qlin_attn_decode for one-token steps (fuse_packed turns it on)
+        self.rope_kernel = False  # qlin_rope_f16 (fuse_packed turns it on)
 
     def fuse_packed(self):
         """q_proj + k_proj + v_proj as one fused packed launch (all read the normed hidden), and
         the fused decode-attention kernel for one-token steps."""
         self.qkv = FusedPackedLinear([self.q_proj, self.k_proj, self.v_proj])
         self.decode_kernel = True
+        self.rope_kernel = hasattr(self.rotary_emb, "cos_cached")
         return self
 
     def _attn_bypassed(self):
@@ -182,6 +184,19 @@ class QuantLlamaAttention(nn.Module):
         if self.qkv is not None and not self.q_proj.use_act_quant:
             return self.qkv(hidden_states)
         return self.q_proj(hidden_states), self.k_proj(hidden_states), self.v_proj(hidden_states)
+
+    def _rope_cache(self, value_states, kv_seq_len):
+        """fp32 views of the rotary cos/sin cache (grown exactly as rotary_emb() grows it); a
+        cache held in fp16 (after .half()) is upcast once, exactly."""
+        rot = self.rotary_emb
+        if kv_seq_len > rot.max_seq_len_cached:
+            rot(value_states, seq_len=kv_seq_len)  # the reference's cache growth
+        c, s_ = rot.cos_cached, rot.sin_cached
+        key = (c.data_ptr(), c.dtype, c.shape)
+        if getattr(self, "_rope32_key", None) != key:
+            self._rope32 = (c.float().contiguous(), s_.float().contiguous())
+            self._rope32_key = key
+        return self._rope32
 
     def _out(self, attn_output, residual):
         if residual is None:
@@ -208,17 +223,22 @@ class QuantLlamaAttention(nn.Module):
         bsz, q_len, _ = hidden_states.size()
         act_dtype = hidden_states.dtype
         q, k, v = self._project(hidden_states)
-        query_states = q.reshape(bsz, q_len, self.num_heads, self.head_dim).transpose(1, 2).type(torch.float32)
-        key_states = k.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
         value_states = v.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
-
-        kv_seq_len = key_states.shape[-2]
+        kv_seq_len = q_len
         if past_key_value is not None:
             kv_seq_len += past_key_value[0].shape[-2]
         if position_ids is None:
             position_ids = torch.arange(kv_seq_len - q_len, kv_seq_len, device=hidden_states.device)[None]
-        cos, sin = self.rotary_emb(value_states, seq_len=kv_seq_len)
-        query_states, key_states = apply_rotary_pos_emb(query_states, key_states, cos, sin, position_ids)
+        if self.rope_kernel and q.dtype == torch.float16 and q.is_cuda:
+            # one launch: reshape/transpose, q -> fp32, cos/sin slice + cast, apply_rotary_pos_emb
+            cos_c, sin_c = self._rope_cache(value_states, kv_seq_len)
+            query_states, key_states = qlin.rope(q, k, cos_c, sin_c, position_ids, self.num_heads,
+                                                 self.num_key_value_heads, self.head_dim)
+        else:
+            query_states = q.reshape(bsz, q_len, self.num_heads, self.head_dim).transpose(1, 2).type(torch.float32)
+            key_states = k.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
+            cos, sin = self.rotary_emb(value_states, seq_len=kv_seq_len)
+            query_states, key_states = apply_rotary_pos_emb(query_states, key_states, cos, sin, position_ids)
 
         if past_key_value is not None:
             key_states = torch.cat([past_key_value[0], key_states], dim=2)
@@ -340,6 +360,8 @@ class QuantLlamaDecoderLayer(nn.Module):
         self.self_attn.fuse_packed()
         self.mlp.fuse_packed()
         self.fused_epilogues = self.self_attn.o_proj.packed and self.mlp.down_proj.packed
+        self.input_layernorm.use_kernel = True
+        self.post_attention_layernorm.use_kernel = True
         return self
 
     @torch.no_grad()

@@ -1,10 +1,14 @@
 """Norm layers of the quantized decoder layers (reference quant/omni_norm.py:11-63).
 
-Not a kernel target: RMSNorm is computed in fp32 and cast back, exactly as
-the reference does, with torch ops on the device.
+RMSNorm is computed in fp32 and cast back, exactly as the reference does, with torch ops on the
+device; in the fused packed decoder layer (``use_kernel``, set by
+``QuantLlamaDecoderLayer.fuse_packed_projections``) it is one gfx950 launch (``qlin_rmsnorm_f16``,
+same arithmetic, sum of squares in another order).
 """
 import torch
 import torch.nn as nn
+
+from . import qlin
 
 
 class OmniLayerNorm(nn.Module):
@@ -39,8 +43,20 @@ class OmniLlamaRMSNorm(nn.Module):
         self.bias = None
         self.variance_epsilon = eps
         self.use_temporary_parameter = False
+        self.use_kernel = False
+        self._w32 = None
+
+    def _kernel_weight(self):
+        w = self.weight
+        if self._w32 is None or self._w32[0] is not w or self._w32[1] != w._version:
+            self._w32 = (w, w._version, w.detach().to(torch.float32).contiguous())
+        return self._w32[2]
 
     def forward(self, hidden_states):
+        if (self.use_kernel and not self.use_temporary_parameter and self.bias is None
+                and hidden_states.is_cuda and hidden_states.dtype == torch.float16):
+            return qlin.rmsnorm(hidden_states.contiguous(), self._kernel_weight(),
+                                self.variance_epsilon)
         input_dtype = hidden_states.dtype
         variance = hidden_states.to(torch.float32).pow(2).mean(-1, keepdim=True)
         hidden_states = hidden_states * torch.rsqrt(variance + self.variance_epsilon)

@@ -47,6 +47,8 @@ SIGNATURES = {
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _p], _i),
+    "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),
+    "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
     "qlin_attn_decode_partials_bytes": ([_l, _i, _i, _l], _l),
     "qlin_attn_decode": ([_p, _p, _p, _p, _p, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p], _i),
 }
@@ -342,6 +344,67 @@ def interleave_gate_up(qw_gate, qsz_gate, qw_up, qsz_up):
     ps = lambda z: z.view(T, G, 2, 8).permute(0, 2, 1, 3)
     qsz = torch.stack([ps(qsz_gate), ps(qsz_up)], dim=3).reshape(2 * T, G, 16)
     return qw.contiguous(), qsz.contiguous()
+
+
+def rmsnorm(x, weight_f32, eps):
+    """``qlin_rmsnorm_f16``: OmniLlamaRMSNorm on fp16 ``x`` [..., H] with the fp32 weight."""
+    _dev(x, weight_f32)
+    if x.dtype != torch.float16 or weight_f32.dtype != torch.float32:
+        raise ValueError("rmsnorm takes fp16 x and an fp32 weight")
+    H = x.shape[-1]
+    if weight_f32.numel() != H:
+        raise ValueError(f"weight has {weight_f32.numel()} values, x has {H} features")
+    y = torch.empty_like(x)
+    rc = load_library().qlin_rmsnorm_f16(_ptr(x), _ptr(weight_f32), _ptr(y), x.numel() // H, H,
+                                         float(eps), _stream(x))
+    _check(rc, "qlin_rmsnorm_f16")
+    return y
+
+
+def _rows(t):
+    """(row stride) of a [B, S, C] tensor whose rows are uniformly strided with unit inner
+    stride, else None."""
+    if t.dim() == 3 and t.stride(2) == 1 and (t.shape[0] == 1 or t.stride(0) == t.shape[1] * t.stride(1)):
+        return t.stride(1)
+    return None
+
+
+def rope(q, k, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim):
+    """``qlin_rope_f16``: q [B, S, Hq*D], k [B, S, Hkv*D] fp16 (row-strided views allowed) ->
+    (q_rot fp32 [B, Hq, S, D], k_rot fp16 [B, Hkv, S, D]) exactly as the reference's
+    ``apply_rotary_pos_emb(q.transpose(1, 2).float(), k.transpose(1, 2), cos, sin, pos)``."""
+    if _rows(q) is None:
+        q = q.contiguous()
+    if _rows(k) is None:
+        k = k.contiguous()
+    for t_ in (q, k, cos_cache, sin_cache, position_ids):
+        if not t_.is_cuda:
+            raise RuntimeError("qlin kernels run on gfx950 only: got a CPU tensor")
+    if q.dtype != torch.float16 or k.dtype != torch.float16:
+        raise ValueError("rope takes fp16 q / k")
+    if cos_cache.dtype != torch.float32 or sin_cache.dtype != torch.float32 or \
+            not cos_cache.is_contiguous() or not sin_cache.is_contiguous():
+        raise ValueError("rope takes contiguous fp32 cos / sin caches")
+    B, S = q.shape[0], q.shape[1]
+    pos = position_ids
+    if pos.dtype != torch.int64:
+        pos = pos.to(torch.int64)
+    if pos.dim() == 1:
+        pos = pos[None]
+    if pos.stride(-1) != 1:
+        pos = pos.contiguous()
+    pbs = pos.stride(0) if pos.shape[0] > 1 else 0
+    if pos.shape[-1] != S or pos.shape[0] not in (1, B):
+        raise ValueError(f"position_ids {tuple(pos.shape)} do not match [B={B}, S={S}]")
+    q_out = torch.empty(B, n_heads, S, head_dim, dtype=torch.float32, device=q.device)
+    k_out = torch.empty(B, n_kv_heads, S, head_dim, dtype=torch.float16, device=q.device)
+    if cos_cache.shape != sin_cache.shape or cos_cache.shape[-1] != head_dim:
+        raise ValueError("cos / sin caches must be [rows, head_dim]")
+    rc = load_library().qlin_rope_f16(_ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(cos_cache),
+                                      _ptr(sin_cache), cos_cache.shape[0], _ptr(pos), pbs, _ptr(q_out), _ptr(k_out),
+                                      B, S, n_heads, n_kv_heads, head_dim, _stream(q))
+    _check(rc, "qlin_rope_f16")
+    return q_out, k_out
 
 
 ATTN_MAX_L = 4096

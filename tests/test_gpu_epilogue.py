@@ -66,3 +66,42 @@ def test_epilogue_argument_checks():
                                   qlin.EP_SILU_MUL, None) == 1  # N % 16
     assert lib.qlin_linear_ep_f16(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 32, 128, 4, 128,
                                   7, None) == 1  # unknown epilogue
+
+
+@pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (3, 768), (5, 14336)])
+def test_rmsnorm_kernel_matches_mirror(rows, H):
+    from quant.omni_norm import OmniLlamaRMSNorm
+    rs = np.random.RandomState(rows + H)
+    x = t((rs.randn(1, rows, H) * 3).astype(np.float16))
+    w = torch.nn.Module()
+    w.weight = torch.nn.Parameter(t((1 + 0.1 * rs.randn(H)).astype(np.float16)), requires_grad=False)
+    norm = OmniLlamaRMSNorm(w, eps=1e-5)
+    ref = norm(x)
+    norm.use_kernel = True
+    got = norm(x)
+    diff = (got.float() - ref.float()).abs()
+    # same fp32 arithmetic; the sum of squares runs in another order than torch's reduction
+    assert bool((diff <= ref.float().abs() * 2.0 ** -10 + 1e-7).all()), float(diff.max())
+    assert (diff > 0).float().mean().item() < 0.02
+
+
+@pytest.mark.parametrize("B,S,strided", [(1, 1, True), (1, 37, True), (3, 5, False), (2, 64, True)])
+def test_rope_kernel_bit_exact(B, S, strided):
+    from models.int_llama_layer import LlamaRotaryEmbedding437, apply_rotary_pos_emb
+    Hq, Hkv, D = 8, 2, 128
+    rs = np.random.RandomState(B * 100 + S)
+    qkv = t((rs.randn(B, S, (Hq + 2 * Hkv) * D) * 2).astype(np.float16))
+    q, k, _ = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
+    if not strided:
+        q, k = q.contiguous(), k.contiguous()
+    rot = LlamaRotaryEmbedding437(D, 256, 500000.0, device="cuda").half()  # cache in fp16, as after layer.half()
+    pos = torch.stack([torch.arange(S) + 11 * b for b in range(B)]).cuda()
+    qs = q.reshape(B, S, Hq, D).transpose(1, 2).type(torch.float32)
+    ks = k.reshape(B, S, Hkv, D).transpose(1, 2)
+    cos, sin = rot(ks, seq_len=int(pos.max()) + 1)
+    ref_q, ref_k = apply_rotary_pos_emb(qs, ks, cos, sin, pos)
+    got_q, got_k = qlin.rope(q, k, rot.cos_cached.float().contiguous(),
+                             rot.sin_cached.float().contiguous(), pos, Hq, Hkv, D)
+    assert got_q.dtype == torch.float32 and got_k.dtype == torch.float16
+    assert torch.equal(got_q, ref_q.contiguous())
+    assert torch.equal(got_k, ref_k.contiguous())

@@ -63,9 +63,11 @@ def test_packed_ppl_matches_fake_quant():
     assert np.isfinite(ppl_fq) and abs(ppl_pk - ppl_fq) / ppl_fq < 1e-3, (ppl_fq, ppl_pk)
 
 
-def test_fused_projections_bit_identical():
-    """q/k/v and gate/up fused into one packed launch each (FusedPackedLinear): every output
-    element takes the same kernel path as unfused, so logits must be bit-identical."""
+def test_fused_layer_matches_unfused():
+    """fuse_packed_projections(): q/k/v and gate/up (+ SiLU·mul) as one launch each, residual
+    adds in the o_proj / down_proj epilogues (all bit-identical per element), RMSNorm and RoPE
+    as single kernels (RoPE bit-exact; RMSNorm's sum of squares in another order: one fp16 ulp
+    here and there), decode attention kernel — logits within 1e-3 relative."""
     cfg = _cfg(layers=2)
     model = build_random_quant_llama(cfg, quant_args(4, 128), seed=13, device="cuda",
                                      dtype=torch.float16)
@@ -79,4 +81,4 @@ def test_fused_projections_bit_identical():
             layer.fuse_packed_projections()
         got = [model(x) for x in toks]
     for a, b in zip(got, ref):
-        assert torch.equal(a, b)
+        assert _rel(a, b) < 1e-3, _rel(a, b)
