@@ -303,10 +303,12 @@ uint32_t group_magic(int group) {
   return (uint32_t)(((1ull << 31) + d - 1) / d);
 }
 
-// waves per block: grow W until the grid holds ~16 waves for each of the 256 CUs
+// waves per block: grow W until the grid holds ~32 waves for each of the 256 CUs (measured on
+// the decode layer's shapes, tools/dev/gemv_geo.py: N = 28,672 x K = 4,096 W = 8 12.6 us vs
+// W = 4 13.3 us; 4096 x 4096 and 6144 x 4096 keep W = 16)
 int pick_waves(int Nt, int Kt, int& tpw) {
   int W = 1;
-  while (W < kMaxWaves && (int64_t)Nt * W < 4096) W *= 2;
+  while (W < kMaxWaves && (int64_t)Nt * W < 8192) W *= 2;
   W = min(W, Kt);
   tpw = (Kt + W - 1) / W;
   return (Kt + tpw - 1) / tpw;

@@ -18,8 +18,62 @@
 
 namespace {
 
-constexpr int kNormThreads = 256;
+using qlin::h8;
 
+constexpr int kNormThreads = 256;
+constexpr int kNormCPT = 4;  // 8-half chunks a thread keeps in registers: H <= 8192
+
+// block sum of a per-thread float (every thread gets the total)
+__device__ __forceinline__ float block_sum(float v, float* part) {
+  v = qlin::row16_sum(v);
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int i = 0; i < kNormThreads / 64; ++i) tot += part[i];
+  return tot;
+}
+
+// H % 8 == 0 and H <= 8 * kNormThreads * kNormCPT: x read once with 16-B loads, kept in registers
+__global__ __launch_bounds__(kNormThreads) void rmsnorm_vec_kernel(
+    const _Float16* __restrict__ x, const float* __restrict__ w, _Float16* __restrict__ y,
+    int H, float eps) {
+#pragma clang fp contract(off)
+  __shared__ float part[kNormThreads / 64];
+  const int64_t row = blockIdx.x;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + row * H);
+  const int nch = H >> 3;
+  uint4 xv[kNormCPT];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < kNormCPT; ++c) {
+    const int ch = c * kNormThreads + threadIdx.x;
+    xv[c] = ch < nch ? xr[ch] : make_uint4(0u, 0u, 0u, 0u);
+    const h8 v = __builtin_bit_cast(h8, xv[c]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += (float)v[j] * (float)v[j];
+  }
+  const float var = block_sum(ss, part) / (float)H;
+  const float r = rsqrtf(var + eps);
+  uint4* yr = reinterpret_cast<uint4*>(y + row * H);
+  const float4* wr = reinterpret_cast<const float4*>(w);
+#pragma unroll
+  for (int c = 0; c < kNormCPT; ++c) {
+    const int ch = c * kNormThreads + threadIdx.x;
+    if (ch >= nch) break;
+    const h8 v = __builtin_bit_cast(h8, xv[c]);
+    const float4 w0 = wr[2 * ch], w1 = wr[2 * ch + 1];
+    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)(wv[j] * ((float)v[j] * r));
+    yr[ch] = __builtin_bit_cast(uint4, o);
+  }
+}
+
+// any H: two passes over the row
 __global__ __launch_bounds__(kNormThreads) void rmsnorm_kernel(
     const _Float16* __restrict__ x, const float* __restrict__ w, _Float16* __restrict__ y,
     int64_t H, float eps) {
@@ -32,16 +86,7 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_kernel(
     const float v = (float)xr[i];
     ss += v * v;
   }
-  // wave sum (rows of 16, then the four row totals), then the block's waves
-  ss = qlin::row16_sum(ss);
-  ss += __shfl_xor(ss, 16);
-  ss += __shfl_xor(ss, 32);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = ss;
-  __syncthreads();
-  float tot = 0.f;
-#pragma unroll
-  for (int i = 0; i < kNormThreads / 64; ++i) tot += part[i];
-  const float var = tot / (float)H;
+  const float var = block_sum(ss, part) / (float)H;
   const float r = rsqrtf(var + eps);
   _Float16* yr = y + row * H;
   for (int64_t i = threadIdx.x; i < H; i += kNormThreads) {
@@ -93,8 +138,14 @@ extern "C" int qlin_rmsnorm_f16(const uint16_t* x, const float* weight, uint16_t
                                 int64_t H, float eps, void* stream) {
   if (!x || !weight || !y || rows < 0 || H <= 0 || rows > 0x7fffffff) return QLIN_EINVAL;
   if (rows == 0) return QLIN_OK;
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3((unsigned)rows), dim3(kNormThreads), 0,
-                     (hipStream_t)stream, (const _Float16*)x, weight, (_Float16*)y, H, eps);
+  const bool vec = H % 8 == 0 && H <= 8 * kNormThreads * kNormCPT &&
+                   ((uintptr_t)x | (uintptr_t)y) % 16 == 0 && (uintptr_t)weight % 16 == 0;
+  if (vec)
+    hipLaunchKernelGGL(rmsnorm_vec_kernel, dim3((unsigned)rows), dim3(kNormThreads), 0,
+                       (hipStream_t)stream, (const _Float16*)x, weight, (_Float16*)y, (int)H, eps);
+  else
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3((unsigned)rows), dim3(kNormThreads), 0,
+                       (hipStream_t)stream, (const _Float16*)x, weight, (_Float16*)y, H, eps);
   return (int)hipGetLastError();
 }
 
