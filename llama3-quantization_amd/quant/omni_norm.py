@@ -2,8 +2,8 @@
 
 RMSNorm is computed in fp32 and cast back, exactly as the reference does, with torch ops on the
 device; in the fused packed decoder layer (``use_kernel``, set by
-``QuantLlamaDecoderLayer.fuse_packed_projections``) it is one gfx950 launch (``qlin_rmsnorm_f16``,
-same arithmetic, sum of squares in another order).
+``QuantLlamaDecoderLayer.fuse_packed_projections``) decode-sized inputs (<= 64 rows) take one
+gfx950 launch (``qlin_rmsnorm_f16``, same arithmetic, sum of squares in another order).
 """
 import torch
 import torch.nn as nn
@@ -36,6 +36,12 @@ class OmniLayerNorm(nn.Module):
         self.use_act_quant = use_act_quant
 
 
+# the kernel serves decode-sized inputs (its sum-of-squares order differs from torch's reduction,
+# so it can move an fp16 ulp); prefill windows keep the reference's torch ops, where the norm is
+# a negligible share of the layer and the fused layer stays bit-identical to the unfused one
+KERNEL_MAX_ROWS = 64
+
+
 class OmniLlamaRMSNorm(nn.Module):
     def __init__(self, ori_norm, eps=1e-6):
         super().__init__()
@@ -54,7 +60,8 @@ class OmniLlamaRMSNorm(nn.Module):
 
     def forward(self, hidden_states):
         if (self.use_kernel and not self.use_temporary_parameter and self.bias is None
-                and hidden_states.is_cuda and hidden_states.dtype == torch.float16):
+                and hidden_states.is_cuda and hidden_states.dtype == torch.float16
+                and hidden_states.numel() <= KERNEL_MAX_ROWS * hidden_states.shape[-1]):
             return qlin.rmsnorm(hidden_states.contiguous(), self._kernel_weight(),
                                 self.variance_epsilon)
         input_dtype = hidden_states.dtype

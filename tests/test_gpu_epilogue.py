@@ -68,7 +68,7 @@ def test_epilogue_argument_checks():
                                   7, None) == 1  # unknown epilogue
 
 
-@pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (3, 768), (5, 14336)])
+@pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (3, 768), (5, 14336), (64, 4096)])
 def test_rmsnorm_kernel_matches_mirror(rows, H):
     from quant.omni_norm import OmniLlamaRMSNorm
     rs = np.random.RandomState(rows + H)

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU-box profiling session for the round's committed evidence (copy gpurun_out/prof_rN/* to
+# profiles/ afterwards): bench lines per workload, rocprofv3 kernel-trace stats of the default
+# bench, the FETCH_SIZE PMC pass (its own run), the decode-layer and full-size PPL parity tools.
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+R=${ROUND:-r1}
+OUT=$ROOT/gpurun_out/prof_$R
+mkdir -p "$OUT"
+step() {  # name, timeout, command...
+  local name=$1 t=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  if [ $rc -ne 0 ]; then echo "STOP: $name exited $rc"; tail -5 "$OUT/$name.err"; exit $rc; fi
+  tail -1 "$OUT/$name.out"
+}
+step bench_gemv_int4_g128 300 python bench.py
+for w in ${WORKLOADS:-gemv_int3_g64 gemv_int2_g64 gemv_int3_g64_hqq gemv_int2_g64_hqq gemm_int4_g128_m32 gemm_int4_g128_m2048 gemm_int4_g128_m65536 gemm_int4_g64_hqq_m2048}; do
+  step bench_$w 300 python bench.py --workload $w --no-cpu-baseline
+done
+export TMPDIR=/tmp
+(cd /tmp && step kernel_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run \
+   -- python "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline) || exit $?
+find "$OUT/kt" -name "*kernel_stats.csv" -exec cp {} "$OUT/${R}_gemv_int4_g128_kernel_stats.csv" \;
+(cd /tmp && step pmc 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run \
+   -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $?
+python tools/pmc_traffic.py "$OUT/pmc" gemv_kernel gemv_int4_g128 "$OUT/${R}_gemv_int4_g128_pmc.json"
+step decode_layer 300 python tools/bench_decode.py
+step ppl_llama3_8b 500 python tools/ppl_llama3_8b.py
+echo "done: $OUT"
