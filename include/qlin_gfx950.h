@@ -143,7 +143,7 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
 
 /*
  * The packed linear with a fused output epilogue (the decoder layer's glue around two of its
- * linears, models/int_llama_layer.py of the reference):
+ * linears, models/int_llama_layer.py of the reference) and optional activation fake-quant:
  *   QLIN_EP_RESIDUAL  y = RN16(residual + RN16(x @ W_dq^T + bias)) — o_proj / down_proj followed
  *                     by `hidden_states = residual + hidden_states` (:241-257); residual [M, N].
  *   QLIN_EP_SILU_MUL  W's rows interleaved in 8-row halves (rows 16j..16j+7 = gate rows
@@ -151,6 +151,12 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
  *                     y[M, N/2] = RN16(RN16(silu(gate)) * up) with gate / up the fp16 F.linear
  *                     outputs — QuantLlamaMLP's act_fn(gate_proj(x)) * up_proj(x) (:44-45).
  *   QLIN_EP_NONE      == qlin_linear_f16.
+ * act_bits != 0 additionally fake-quantizes x per token first — QuantLinear.forward's
+ * act_quantizer(input) (quant/int_linear.py:59-60) with UniformAffineQuantizer(n_bits=act_bits,
+ * dynamic_method="per_token") (quant/quantizer.py:132-159, :94-115), bit-exact; act_flags takes
+ * QLIN_SYMMETRIC / QLIN_DISABLE_ZERO_POINT.  M <= 64: fused into the GEMV (each block recomputes
+ * the token's min / max; x 16-byte aligned, K % 8 == 0); M > 64: the quantizer kernel writes
+ * x_dq to `workspace` (fp16 [M, K], required) before the GEMM.
  * Same kernels and dispatch as qlin_linear_f16 (GEMV for M <= 64, MFMA GEMM above).
  */
 #define QLIN_EP_NONE     0
@@ -158,7 +164,8 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
 #define QLIN_EP_SILU_MUL 2
 int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                        const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M,
-                       int64_t N, int64_t K, int bits, int group, int epilogue, void* stream);
+                       int64_t N, int64_t K, int bits, int group, int epilogue, int act_bits,
+                       int act_flags, uint16_t* workspace, void* stream);
 
 /*
  * Fused decode attention (one query token per sequence), for the quantized LLaMA layer's

@@ -268,6 +268,57 @@ __device__ __forceinline__ void dequant_step(const Piece<BITS>& c, const Magics&
 }
 
 // ---------------------------------------------------------------------------------------------
+// the reference quantizer's arithmetic (quant/quantizer.py), shared by the quantizer kernels and
+// the GEMV's fused per-token activation fake-quant
+// ---------------------------------------------------------------------------------------------
+struct QP {
+  int64_t rows;
+  int K, group, cpr, cpg, rpb, bits, flags;
+  float qmin, qmax;
+};
+
+// (scale, zp) of one group — quant/quantizer.py:141-159
+template <typename T>
+__device__ __forceinline__ void calib(float xmin, float xmax, float up, float low, const QP& P,
+                                      float& scale, float& zp) {
+#pragma clang fp contract(off)
+  using E = Elt<T>;
+  if (P.flags & QLIN_LWC) {
+    xmax = E::rn(up * xmax);
+    xmin = E::rn(low * xmin);
+  }
+  if (P.flags & QLIN_SYMMETRIC) {
+    const float am = max_nan(fabsf(xmax), fabsf(xmin));
+    scale = E::rn(am / (float)((1 << (P.bits - 1)) - 1));
+    scale = E::rn(clamp_nan(scale, 1e-5f, 1e4f));
+    zp = (float)((1 << (P.bits - 1)) - 1);
+  } else {
+    const float range = E::rn(xmax - xmin);
+    scale = E::rn(range / (float)((1 << P.bits) - 1));
+    scale = E::rn(clamp_nan(scale, 1e-5f, 1e4f));
+    zp = E::rn(-xmin / scale);
+  }
+  zp = rintf(E::rn(clamp_nan(zp, -1e4f, 1e4f)));
+}
+
+// fake_quant of one element — quant/quantizer.py:103-110 (round_ste forward = (r - v) + v)
+template <typename T>
+__device__ __forceinline__ float fq(float x, float s, float zp, bool has_zp, const QP& P,
+                                    float& xi_out) {
+#pragma clang fp contract(off)
+  using E = Elt<T>;
+  const float v = E::rn(x / s);
+  const float r = rintf(v);
+  float xi = E::rn(E::rn(r - v) + v);
+  if (has_zp) xi = E::rn(xi + zp);
+  xi = clamp_nan(xi, P.qmin, P.qmax);
+  xi_out = xi;
+  float d = xi;
+  if (has_zp) d = E::rn(d - zp);
+  return E::rn(d * s);
+}
+
+// ---------------------------------------------------------------------------------------------
 // wave64 reductions (DPP within 16-lane rows, then the four row totals)
 // ---------------------------------------------------------------------------------------------
 template <int CTRL>
@@ -296,9 +347,11 @@ constexpr int kEpResidual = 1;
 constexpr int kEpSiluMul = 2;
 
 // the GEMV kernel with an output epilogue (qlin_gemv.hip), for qlin_linear_ep_f16
+// (act_bits != 0: per-token activation fake-quant of x with the quantizer flags act_flags)
 int gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
             const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
-            int64_t K, int bits, int group, int epilogue, void* stream);
+            int64_t K, int bits, int group, int epilogue, int act_bits, int act_flags,
+            void* stream);
 
 // torch's fp32 silu (x / (1 + exp(-x))) on an fp16 value, rounded to fp16
 __device__ __forceinline__ float silu_rn16(float g) {

@@ -403,10 +403,12 @@ extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int
 extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                                   const uint16_t* x, const uint16_t* bias,
                                   const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
-                                  int64_t K, int bits, int group, int epilogue, void* stream) {
+                                  int64_t K, int bits, int group, int epilogue, int act_bits,
+                                  int act_flags, uint16_t* workspace, void* stream) {
   if (epilogue < kEpNone || epilogue > kEpSiluMul) return QLIN_EINVAL;
   if (epilogue == kEpResidual && !residual) return QLIN_EINVAL;
   if (epilogue == kEpSiluMul && N % kTileN) return QLIN_EINVAL;
+  if (act_bits && (act_bits < 2 || act_bits > 8)) return QLIN_EINVAL;
   if (M < 0) return QLIN_EINVAL;
   if (M == 0) return QLIN_OK;
   const int64_t ny = epilogue == kEpSiluMul ? N / 2 : N;  // columns of y (and residual)
@@ -415,10 +417,18 @@ extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, 
       const int64_t mc = M - m0 < 16 ? M - m0 : 16;
       const int rc = qlin::gemv_ep(qweight, qsz, flags, x + m0 * K, bias,
                                    residual ? residual + m0 * ny : nullptr, y + m0 * ny, mc, N, K,
-                                   bits, group, epilogue, stream);
+                                   bits, group, epilogue, act_bits, act_flags, stream);
       if (rc) return rc;
     }
     return QLIN_OK;
+  }
+  if (act_bits) {  // batched tokens: the quantizer kernel writes x_dq into the workspace first
+    if (!workspace) return QLIN_EINVAL;
+    const int rc = qlin_quantize(x, QLIN_F16, M, K, act_bits, (int)K,
+                                 act_flags & (QLIN_SYMMETRIC | QLIN_DISABLE_ZERO_POINT), nullptr,
+                                 nullptr, workspace, nullptr, nullptr, nullptr, nullptr, stream);
+    if (rc) return rc;
+    x = workspace;
   }
   return gemm_ep(qweight, qsz, flags, x, bias, residual, y, M, N, K, bits, group, epilogue,
                  stream);

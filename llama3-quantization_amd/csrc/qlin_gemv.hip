@@ -38,9 +38,19 @@ namespace {
 
 constexpr int kMaxWaves = 16;
 
-struct Ep {  // output epilogue (qlin_common.h kEp*)
+// per-token activation fake-quant of x fused into the GEMV (UniformAffineQuantizer with
+// dynamic_method="per_token", quant/quantizer.py:132-159 + :94-115, as QuantLinear.forward's
+// act_quantizer(input) at quant/int_linear.py:59-60): every block recomputes each row's min / max
+// over K (x is L2-resident: 2 B x K per row) and fake-quantizes the x values it parks
+struct ActQ {
+  int on, bits, flags;
+  float qmin, qmax;
+};
+
+struct Ep {  // output epilogue (qlin_common.h kEp*) and fused activation fake-quant
   const uint16_t* res;
   int ep;
+  ActQ aq;
 };
 constexpr int kGemvMaxM = 16;  // one MFMA row block
 
@@ -100,6 +110,26 @@ __device__ __forceinline__ void load_x(XRaw<MT>& r, const Geo& g, int kt) {
 
 // park a tile's x in the wave's LDS slot (row m at words 64m .. 64m+63), read back the A
 // fragments of its 4 k-steps: lane (m = n_in, q) takes row min(m, MT-1) at k = 32s + 8q .. +7
+// fake-quantize the 2*MT halfs of a lane's raw x words (row `row` of x), the reference's fp16
+// arithmetic (qlin_common.h fq)
+template <int MT>
+__device__ __forceinline__ void fake_quant_x(XRaw<MT>& r, const ActQ& aq, float sc, float zp) {
+  QP P;
+  P.bits = aq.bits;
+  P.flags = aq.flags;
+  P.qmin = aq.qmin;
+  P.qmax = aq.qmax;
+  const bool has_zp = !(aq.flags & QLIN_DISABLE_ZERO_POINT);
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const h2 v = as_h2(r.w[i]);
+    float xi;
+    const float lo = fq<_Float16>((float)v.x, sc, zp, has_zp, P, xi);
+    const float hi = fq<_Float16>((float)v.y, sc, zp, has_zp, P, xi);
+    r.w[i] = as_u32(h2{(_Float16)lo, (_Float16)hi});
+  }
+}
+
 template <int MT>
 __device__ __forceinline__ void park_x(h8 (&xa)[4], const XRaw<MT>& r, uint32_t* slot, int lane,
                                        int n_in) {
@@ -121,7 +151,8 @@ __device__ __forceinline__ void park_x(h8 (&xa)[4], const XRaw<MT>& r, uint32_t*
 
 template <int BITS, int MT, int GPT, int ZM, int PF>
 __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0, int nts,
-                                          int ktl, f4& acc) {
+                                          int ktl, f4& acc, const ActQ& aq, float aq_sc,
+                                          float aq_zp) {
   const Magics mg = make_magics<BITS>();
 
   // FULL: the tile is not the matrix's last (only that one can hold fewer than 4 k-steps)
@@ -138,8 +169,9 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, acc, 0, 0, 0);
     }
   };
-  auto tile = [&](const WTile<BITS, GPT>& t, const XRaw<MT>& xr, int kt, auto FULL_) {
+  auto tile = [&](const WTile<BITS, GPT>& t, XRaw<MT>& xr, int kt, auto FULL_) {
     h8 xa[4];
+    if (aq.on) fake_quant_x<MT>(xr, aq, aq_sc, aq_zp);  // wave-uniform
     park_x<MT>(xa, xr, xslot, g.lane, g.n_in);
     step(t, xa, kt, std::integral_constant<int, 0>{}, FULL_);
     step(t, xa, kt, std::integral_constant<int, 1>{}, FULL_);
@@ -185,9 +217,10 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
     int M, int N, int K, int group, uint32_t gmagic, int tpw, const _Float16* __restrict__ res,
-    int ep) {
+    int ep, ActQ aq) {
   __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
+  __shared__ float aq_s[2][MT];
   const int W = blockDim.x >> 6;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
@@ -209,8 +242,50 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
   const int nts = max(0, min(tpw, Kt - kt0));
   const int ktl = max(0, min(Kt - 1, kt0 + nts - 1));
 
+  float aq_sc = 0.f, aq_zp = 0.f;
+  if (aq.on) {  // per-row (token) min / max over K, then the reference's calibration
+#pragma clang fp contract(off)
+    float* mm = red;  // [MT][2][kMaxWaves] scratch, free until the partial sums
+    const int nch = K >> 3;
+    for (int m = 0; m < M; ++m) {
+      float mn = __builtin_inff(), mx = -__builtin_inff();
+      for (int c = tid; c < nch; c += blockDim.x) {
+        const h8 v = __builtin_bit_cast(h8, reinterpret_cast<const uint4*>(x + (int64_t)m * K)[c]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { mn = min_nan(mn, (float)v[j]); mx = max_nan(mx, (float)v[j]); }
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        mn = min_nan(mn, __shfl_xor(mn, o));
+        mx = max_nan(mx, __shfl_xor(mx, o));
+      }
+      if (g.lane == 0) { mm[(m * 2) * kMaxWaves + wave] = mn; mm[(m * 2 + 1) * kMaxWaves + wave] = mx; }
+    }
+    __syncthreads();
+    if (tid < M) {
+      float mn = mm[(tid * 2) * kMaxWaves], mx = mm[(tid * 2 + 1) * kMaxWaves];
+      for (int w = 1; w < W; ++w) {
+        mn = min_nan(mn, mm[(tid * 2) * kMaxWaves + w]);
+        mx = max_nan(mx, mm[(tid * 2 + 1) * kMaxWaves + w]);
+      }
+      QP P;
+      P.bits = aq.bits;
+      P.flags = aq.flags;
+      P.qmin = aq.qmin;
+      P.qmax = aq.qmax;
+      float sc, zp;
+      calib<_Float16>((float)(_Float16)mn, (float)(_Float16)mx, 1.f, 1.f, P, sc, zp);
+      aq_s[0][tid] = sc;
+      aq_s[1][tid] = zp;
+    }
+    __syncthreads();
+    const int r = min(g.lane / (64 / MT), M - 1);  // the x row this lane parks
+    aq_sc = aq_s[0][r];
+    aq_zp = aq_s[1][r];
+  }
+
   f4 acc = {0.f, 0.f, 0.f, 0.f};
-  gemv_body<BITS, MT, GPT, ZM, PF>(g, &xs[wave][0], kt0, nts, ktl, acc);
+  gemv_body<BITS, MT, GPT, ZM, PF>(g, &xs[wave][0], kt0, nts, ktl, acc, aq, aq_sc, aq_zp);
 
   // combine the W partials of each (row m < MT, column n): C row m = 4q + i sits in lane
   // n + 16q, element i; layout [m][n][wave] so one thread reads its 16 partials with 4
@@ -325,7 +400,7 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
 #define QLIN_GV(PF)                                                                        \
   hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, ZM, PF>), dim3(Nt), dim3(64 * W), \
                      0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias,             \
-                     (_Float16*)y, M, N, K, group, gs, tpw, (const _Float16*)e.res, e.ep)
+                     (_Float16*)y, M, N, K, group, gs, tpw, (const _Float16*)e.res, e.ep, e.aq)
   if constexpr (MT >= 8) {  // x registers of 4 tiles in flight would spill
     QLIN_GV(2);
   } else {
@@ -386,14 +461,21 @@ extern "C" int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, in
 }
 
 // GEMV with an output epilogue (qlin_linear_ep_f16's M <= 16 leg)
-int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags,
-                                     const uint16_t* x, const uint16_t* bias,
-                                     const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
-                                     int64_t K, int bits, int group, int epilogue, void* stream) {
+int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
+                  const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M,
+                  int64_t N, int64_t K, int bits, int group, int epilogue, int act_bits,
+                  int act_flags, void* stream) {
   if (!qweight || !qsz || !x || !y || M < 1 || M > kGemvMaxM || !valid_layout(N, K, bits, group))
     return QLIN_EINVAL;
+  if (act_bits && (act_bits < 2 || act_bits > 8 || K % 8 || ((uintptr_t)x & 15))) return QLIN_EINVAL;
   if (N == 0) return QLIN_OK;
-  const Ep e{residual, epilogue};
+  ActQ aq{act_bits != 0, act_bits, act_flags, 0.f, 0.f};
+  if (aq.on) {
+    const bool has_zp = !(act_flags & QLIN_DISABLE_ZERO_POINT);
+    aq.qmin = has_zp ? 0.f : -(float)(1 << (act_bits - 1));
+    aq.qmax = has_zp ? (float)((1 << act_bits) - 1) : (float)((1 << (act_bits - 1)) - 1);
+  }
+  const Ep e{residual, epilogue, aq};
   hipStream_t st = (hipStream_t)stream;
   const int m = (int)M, n = (int)N, k = (int)K;
   const int zm = zero_mode(flags);
@@ -414,5 +496,5 @@ extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int f
                              const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
                              int64_t N, int64_t K, int bits, int group, void* stream) {
   return qlin::gemv_ep(qweight, qsz, flags, x, bias, nullptr, y, M, N, K, bits, group,
-                               kEpNone, stream);
+                               kEpNone, 0, 0, stream);
 }

@@ -21,11 +21,6 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxChunks = 1024;  // chunks per block: K <= 32768
 
-struct QP {
-  int64_t rows;
-  int K, group, cpr, cpg, rpb, bits, flags;
-  float qmin, qmax;
-};
 
 template <typename T>
 __device__ __forceinline__ void load32(const T* __restrict__ p, float (&v)[32]) {
@@ -96,47 +91,6 @@ __device__ __forceinline__ void pack_piece(const uint32_t (&u)[32], uint32_t* __
   }
 #pragma unroll
   for (int i = 0; i < BITS; ++i) out[i] = w[i];
-}
-
-// (scale, zp) of one group — quant/quantizer.py:141-159
-template <typename T>
-__device__ __forceinline__ void calib(float xmin, float xmax, float up, float low, const QP& P,
-                                      float& scale, float& zp) {
-#pragma clang fp contract(off)
-  using E = Elt<T>;
-  if (P.flags & QLIN_LWC) {
-    xmax = E::rn(up * xmax);
-    xmin = E::rn(low * xmin);
-  }
-  if (P.flags & QLIN_SYMMETRIC) {
-    const float am = max_nan(fabsf(xmax), fabsf(xmin));
-    scale = E::rn(am / (float)((1 << (P.bits - 1)) - 1));
-    scale = E::rn(clamp_nan(scale, 1e-5f, 1e4f));
-    zp = (float)((1 << (P.bits - 1)) - 1);
-  } else {
-    const float range = E::rn(xmax - xmin);
-    scale = E::rn(range / (float)((1 << P.bits) - 1));
-    scale = E::rn(clamp_nan(scale, 1e-5f, 1e4f));
-    zp = E::rn(-xmin / scale);
-  }
-  zp = rintf(E::rn(clamp_nan(zp, -1e4f, 1e4f)));
-}
-
-// fake_quant of one element — quant/quantizer.py:103-110 (round_ste forward = (r - v) + v)
-template <typename T>
-__device__ __forceinline__ float fq(float x, float s, float zp, bool has_zp, const QP& P,
-                                    float& xi_out) {
-#pragma clang fp contract(off)
-  using E = Elt<T>;
-  const float v = E::rn(x / s);
-  const float r = rintf(v);
-  float xi = E::rn(E::rn(r - v) + v);
-  if (has_zp) xi = E::rn(xi + zp);
-  xi = clamp_nan(xi, P.qmin, P.qmax);
-  xi_out = xi;
-  float d = xi;
-  if (has_zp) d = E::rn(d - zp);
-  return E::rn(d * s);
 }
 
 template <typename T, int BITS>  // BITS == 0: no packed output

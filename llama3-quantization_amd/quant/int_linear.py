@@ -75,10 +75,24 @@ class QuantLinear(nn.Module):
             bias = self.bias
 
         if self.use_act_quant and not self.disable_input_quant:
+            if self.packed and self._fused_act_bits(input):
+                # per-token fake-quant of x inside the packed linear (bit-exact; the act
+                # quantizer's scale / round_zero_point attributes are not refreshed)
+                return self._packed_fwd(input, weight, bias,
+                                        act_bits=self.act_quantizer.n_bits,
+                                        act_flags=self.act_quantizer._flags())
             input = self.act_quantizer(input)
 
         out = self.fwd_func(input, weight, bias, **self.fwd_kwargs)
         return out
+
+    def _fused_act_bits(self, x):
+        """The act quantizer is the reference's per-token dynamic one (quant/int_linear.py:38-41,
+        main.py act_quant_params) and can run inside the packed linear."""
+        q = self.act_quantizer
+        return (q is not None and q.enable and q.n_bits < 16 and q.dynamic_method == "per_token"
+                and not q.group_size and not q.lwc and q.metric != "fix0to1"
+                and x.dtype == torch.float16 and x.shape[-1] % 8 == 0)
 
     def set_quant_state(self, weight_quant: bool = False, act_quant: bool = False):
         self.use_weight_quant = weight_quant
@@ -87,13 +101,18 @@ class QuantLinear(nn.Module):
     # ------------------------------------------------------------------------------------------
     # packed (real-quant) mode
     # ------------------------------------------------------------------------------------------
-    def _packed_fwd(self, input, weight, bias):
+    def _packed_fwd(self, input, weight, bias, act_bits=0, act_flags=0):
         x = input
         if x.dtype != torch.float16:
             x = x.to(torch.float16)
-        y = qlin.linear(x.contiguous(), self.qweight, self.qsz,
-                        None if bias is None else bias.to(torch.float16).contiguous(),
-                        self.out_features, self.in_features, self.wbits, self.group, self.qflags)
+        b = None if bias is None else bias.to(torch.float16).contiguous()
+        if act_bits:
+            y = qlin.linear_ep(x.contiguous(), self.qweight, self.qsz, b, self.out_features,
+                               self.in_features, self.wbits, self.group, self.qflags,
+                               act_bits=act_bits, act_flags=act_flags)
+        else:
+            y = qlin.linear(x.contiguous(), self.qweight, self.qsz, b, self.out_features,
+                            self.in_features, self.wbits, self.group, self.qflags)
         return y if input.dtype == torch.float16 else y.to(input.dtype)
 
     def _install(self, out, bits, group, keep_weight):

@@ -46,7 +46,8 @@ SIGNATURES = {
     "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
-    "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _p], _i),
+    "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _i, _i, _p, _p],
+                           _i),
     "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),
     "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
     "qlin_attn_decode_partials_bytes": ([_l, _i, _i, _l], _l),
@@ -295,18 +296,20 @@ def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0):
                         extra=(None,))
 
 
+SKINNY_MAX_M = 64  # qlin_linear_*: M <= this runs the GEMV kernel
 EP_NONE = 0
 EP_RESIDUAL = 1
 EP_SILU_MUL = 2
 
 
 def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NONE,
-              residual=None):
+              residual=None, act_bits=0, act_flags=0):
     """``qlin_linear_ep_f16``: the packed linear with a fused output epilogue.
 
     EP_RESIDUAL: ``residual + F.linear(x)`` (residual fp16, shape of the output).
     EP_SILU_MUL: rows interleaved by ``interleave_gate_up``; returns ``silu(gate) * up`` with
-    N / 2 columns."""
+    N / 2 columns.
+    act_bits: per-token activation fake-quant of x first (fused into the GEMV for M <= 64)."""
     _dev(x, qweight, qsz, bias, residual)
     if x.dtype != torch.float16:
         raise ValueError(f"packed linear takes fp16 activations, got {x.dtype}")
@@ -323,9 +326,12 @@ def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NON
     M = x.numel() // K if K else 0
     if M == 0:
         return y
+    ws = None
+    if act_bits and M > SKINNY_MAX_M:
+        ws = torch.empty(M, K, dtype=torch.float16, device=x.device)
     rc = load_library().qlin_linear_ep_f16(_ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(bias),
                                            _ptr(residual), _ptr(y), M, N, K, bits, group,
-                                           epilogue, _stream(x))
+                                           epilogue, act_bits, act_flags, _ptr(ws), _stream(x))
     _check(rc, "qlin_linear_ep_f16")
     return y
 

@@ -60,12 +60,13 @@ def test_epilogue_argument_checks():
     x = t(rand_x(1, 128, 9))
     y = torch.empty(1, 32, dtype=torch.float16, device="cuda")
     P = lambda a: a.data_ptr()
-    assert lib.qlin_linear_ep_f16(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 32, 128, 4, 128,
-                                  qlin.EP_RESIDUAL, None) == 1  # residual missing
-    assert lib.qlin_linear_ep_f16(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 24, 128, 4, 128,
-                                  qlin.EP_SILU_MUL, None) == 1  # N % 16
-    assert lib.qlin_linear_ep_f16(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 32, 128, 4, 128,
-                                  7, None) == 1  # unknown epilogue
+    ep = lib.qlin_linear_ep_f16
+    assert ep(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 32, 128, 4, 128, qlin.EP_RESIDUAL,
+              0, 0, None, None) == 1  # residual missing
+    assert ep(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 24, 128, 4, 128, qlin.EP_SILU_MUL,
+              0, 0, None, None) == 1  # N % 16
+    assert ep(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 32, 128, 4, 128, 7,
+              0, 0, None, None) == 1  # unknown epilogue
 
 
 @pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (3, 768), (5, 14336), (64, 4096)])
@@ -105,3 +106,41 @@ def test_rope_kernel_bit_exact(B, S, strided):
     assert got_q.dtype == torch.float32 and got_k.dtype == torch.float16
     assert torch.equal(got_q, ref_q.contiguous())
     assert torch.equal(got_k, ref_k.contiguous())
+
+
+@pytest.mark.parametrize("M", (1, 2, 5, 16, 33, 200))
+@pytest.mark.parametrize("abits,aflags", [(8, 0), (4, 0), (6, 1), (8, 2)])
+def test_fused_act_quant_matches_two_launches(M, abits, aflags):
+    """qlin_linear_ep_f16 with act_bits: per-token fake-quant of x fused into the GEMV (M <= 64)
+    or run by the quantizer kernel into the workspace (M > 64) — bit-identical to the reference
+    order act_quantizer(x) (quantizer kernel, itself bit-exact with the reference) then the
+    packed linear."""
+    N, K = 272, 1024
+    qw, qsz, fl = _packed(N, K, 11)
+    x = t((np.random.RandomState(M + abits).randn(M, K) * 2).astype(np.float16))
+    xdq = qlin.quantize(x, abits, K, aflags, want_params=False)["x_dq"]
+    ref = qlin.linear(xdq, qw, qsz, None, N, K, 4, 128, fl)
+    got = qlin.linear_ep(x, qw, qsz, None, N, K, 4, 128, fl, act_bits=abits, act_flags=aflags)
+    assert torch.equal(got, ref)
+
+
+def test_quantlinear_act_quant_fused_path(golden):
+    """QuantLinear (packed, W4 + per-token A8) equals the two-launch path on the reference's own
+    A8 activation fixture."""
+    from quant.int_linear import QuantLinear
+    g = golden("q_a8tok_f16")
+    x = t(g["x"])
+    K = x.shape[-1]
+    lin = torch.nn.Linear(K, 64, bias=False).cuda().half()
+    with torch.no_grad():
+        lin.weight.copy_(t(rand_weight(64, K, 3)))
+    ql = QuantLinear(lin, dict(n_bits=4, group_size=min(128, K), dynamic_method="per_channel",
+                               per_channel_axes=[0]),
+                     dict(n_bits=8, per_channel_axes=[], symmetric=False,
+                          dynamic_method="per_token")).cuda()
+    ql.pack_from_weight()
+    ql.set_quant_state(weight_quant=False, act_quant=True)
+    got = ql(x)
+    ref = qlin.linear(t(g["x_dq"]).reshape(-1, K), ql.qweight, ql.qsz, None, 64, K, 4, ql.group,
+                      ql.qflags).reshape(got.shape)
+    assert torch.equal(got, ref)
