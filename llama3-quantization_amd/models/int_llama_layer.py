@@ -19,8 +19,8 @@ import torch
 from torch import nn
 
 from quant import qlin
-from quant.int_linear import (FusedPackedLinear, QuantLinear, SiluMulPackedLinear,
-                              packed_residual_linear)
+from quant.int_linear import (FusedPackedLinear, QuantLinear, SiluMulPackedLinear, _same_act,
+                              act_spec, packed_residual_linear)
 from quant.int_matmul import QuantMatMul
 from quant.omni_norm import OmniLlamaRMSNorm
 
@@ -111,17 +111,20 @@ class QuantLlamaMLP(nn.Module):
         return self
 
     def fused(self):
+        """Fused packed launches apply (their per-token act quantizers, if any, fuse too)."""
         return (self.gate_up is not None or self.gate_up_act is not None) and \
-            not self.gate_proj.use_act_quant
+            _same_act([self.gate_proj, self.up_proj]) is not None and \
+            act_spec(self.down_proj) is not None
 
     def forward(self, x, residual=None):
         """``down(act(gate(x)) * up(x))``; with ``residual`` (fused packed mode only) the
         decoder layer's ``residual + mlp(x)`` is folded into down_proj's epilogue."""
         if self.fused():
+            act = _same_act([self.gate_proj, self.up_proj])
             if self.gate_up_act is not None:
-                h = self.gate_up_act(x)
+                h = self.gate_up_act(x, act)
             else:
-                gate, up = self.gate_up(x)
+                gate, up = self.gate_up(x, act)
                 h = self.act_fn(gate) * up
             if residual is not None:
                 return packed_residual_linear(self.down_proj, h, residual)
@@ -181,8 +184,10 @@ class QuantLlamaAttention(nn.Module):
         return True
 
     def _project(self, hidden_states):
-        if self.qkv is not None and not self.q_proj.use_act_quant:
-            return self.qkv(hidden_states)
+        if self.qkv is not None:
+            act = _same_act([self.q_proj, self.k_proj, self.v_proj])
+            if act is not None:
+                return self.qkv(hidden_states, act)
         return self.q_proj(hidden_states), self.k_proj(hidden_states), self.v_proj(hidden_states)
 
     def _rope_cache(self, value_states, kv_seq_len):
@@ -201,7 +206,7 @@ class QuantLlamaAttention(nn.Module):
     def _out(self, attn_output, residual):
         if residual is None:
             return self.o_proj(attn_output)
-        if self.o_proj.packed and not self.o_proj.use_act_quant:
+        if self.o_proj.packed and act_spec(self.o_proj) is not None:
             return packed_residual_linear(self.o_proj, attn_output, residual)
         return residual + self.o_proj(attn_output)
 

@@ -89,10 +89,7 @@ class QuantLinear(nn.Module):
     def _fused_act_bits(self, x):
         """The act quantizer is the reference's per-token dynamic one (quant/int_linear.py:38-41,
         main.py act_quant_params) and can run inside the packed linear."""
-        q = self.act_quantizer
-        return (q is not None and q.enable and q.n_bits < 16 and q.dynamic_method == "per_token"
-                and not q.group_size and not q.lwc and q.metric != "fix0to1"
-                and x.dtype == torch.float16 and x.shape[-1] % 8 == 0)
+        return act_spec(self) is not None and x.dtype == torch.float16 and x.shape[-1] % 8 == 0
 
     def set_quant_state(self, weight_quant: bool = False, act_quant: bool = False):
         self.use_weight_quant = weight_quant
@@ -182,6 +179,26 @@ class QuantLinear(nn.Module):
         return s
 
 
+def act_spec(lin):
+    """(act_bits, act_flags) for the packed kernels' fused per-token activation fake-quant:
+    (0, 0) when ``lin`` quantizes no activations, None when its act quantizer cannot be fused
+    (not per-token dynamic, grouped, LWC, fix0to1)."""
+    if not lin.use_act_quant or lin.disable_input_quant:
+        return (0, 0)
+    q = lin.act_quantizer
+    if q is None or not q.enable or q.n_bits >= 16:
+        return (0, 0)
+    if (q.dynamic_method == "per_token" and not q.group_size and not q.lwc
+            and q.metric != "fix0to1" and lin.in_features % 8 == 0):
+        return (q.n_bits, q._flags())
+    return None
+
+
+def _same_act(members):
+    specs = [act_spec(m) for m in members]
+    return specs[0] if all(sp == specs[0] for sp in specs) else None
+
+
 class FusedPackedLinear(nn.Module):
     """Several packed QuantLinear that read the same input (q/k/v, gate/up) as ONE fused
     dequant-GEMV/GEMM launch over their concatenated rows.
@@ -218,10 +235,12 @@ class FusedPackedLinear(nn.Module):
         else:
             self.bias = None
 
-    def forward(self, x):
+    def forward(self, x, act=(0, 0)):
+        """``act``: (act_bits, act_flags) of the members' shared per-token act quantizer."""
         xin = x if x.dtype == torch.float16 else x.to(torch.float16)
-        y = qlin.linear(xin.contiguous(), self.qweight, self.qsz, self.bias, self.out_features,
-                        self.in_features, self.wbits, self.group, self.qflags)
+        y = qlin.linear_ep(xin.contiguous(), self.qweight, self.qsz, self.bias, self.out_features,
+                           self.in_features, self.wbits, self.group, self.qflags,
+                           act_bits=act[0], act_flags=act[1])
         if x.dtype != torch.float16:
             y = y.to(x.dtype)
         return torch.split(y, self.splits, dim=-1)
@@ -260,11 +279,12 @@ class SiluMulPackedLinear(nn.Module):
         else:
             self.bias = None
 
-    def forward(self, x):
+    def forward(self, x, act=(0, 0)):
         xin = x if x.dtype == torch.float16 else x.to(torch.float16)
         y = qlin.linear_ep(xin.contiguous(), self.qweight, self.qsz, self.bias,
                            2 * self.out_features, self.in_features, self.wbits, self.group,
-                           self.qflags, epilogue=qlin.EP_SILU_MUL)
+                           self.qflags, epilogue=qlin.EP_SILU_MUL, act_bits=act[0],
+                           act_flags=act[1])
         return y if x.dtype == torch.float16 else y.to(x.dtype)
 
 
@@ -273,6 +293,10 @@ def packed_residual_linear(lin, x, residual):
     decoder layer's residual add fused into o_proj / down_proj's output."""
     xin = x if x.dtype == torch.float16 else x.to(torch.float16)
     bias = None if lin.bias is None else lin.bias.to(torch.float16).contiguous()
+    act = act_spec(lin)
+    if act is None:
+        raise ValueError("the act quantizer of this linear cannot be fused")
     return qlin.linear_ep(xin.contiguous(), lin.qweight, lin.qsz, bias, lin.out_features,
                           lin.in_features, lin.wbits, lin.group, lin.qflags,
-                          epilogue=qlin.EP_RESIDUAL, residual=residual.contiguous())
+                          epilogue=qlin.EP_RESIDUAL, residual=residual.contiguous(),
+                          act_bits=act[0], act_flags=act[1])

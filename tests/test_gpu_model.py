@@ -82,3 +82,26 @@ def test_fused_layer_matches_unfused():
         got = [model(x) for x in toks]
     for a, b in zip(got, ref):
         assert _rel(a, b) < 1e-3, _rel(a, b)
+
+
+def test_fused_layer_w4a8_matches_unfused():
+    """W4A8 (per-token 8-bit activations, the reference's act_quant_params): the fused layer
+    runs the act quantizers inside the packed launches — logits equal the unfused packed path
+    (act quantizer kernel, then the packed linear) within 1e-3 relative."""
+    cfg = _cfg(layers=2)
+    model = build_random_quant_llama(cfg, quant_args(4, 128, abits=8), seed=14, device="cuda",
+                                     dtype=torch.float16)
+    rtn_quantize_(model, pack=True)
+    assert all(m.use_act_quant for layer in model.layers for m in layer.modules()
+               if isinstance(m, QuantLinear))
+    g = torch.Generator(device="cuda").manual_seed(7)
+    toks = [torch.randint(0, cfg.vocab_size, (1, T), device="cuda", generator=g)
+            for T in (1, 9, 80)]
+    with torch.no_grad():
+        ref = [model(x) for x in toks]
+        for layer in model.layers:
+            layer.fuse_packed_projections()
+        assert model.layers[0].mlp.fused()
+        got = [model(x) for x in toks]
+    for a, b in zip(got, ref):
+        assert _rel(a, b) < 1e-3, _rel(a, b)
