@@ -23,9 +23,19 @@ extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
   return (int)hipGetLastError();
 }
 
-// the lab library does not link the GEMV: qlin_linear_f16's skinny branch is never taken here
+// the lab library does not link the GEMV or the quantizer: the skinny / act-quant branches of
+// qlin_linear_*_f16 are never taken here
+int qlin::gemv_ep(const uint32_t*, const uint32_t*, int, const uint16_t*, const uint16_t*,
+                  const uint16_t*, uint16_t*, int64_t, int64_t, int64_t, int, int, int, int, int,
+                  void*) {
+  return QLIN_EINVAL;
+}
 extern "C" int qlin_gemv_f16(const uint32_t*, const uint32_t*, int, const uint16_t*,
                              const uint16_t*, uint16_t*, int64_t, int64_t, int64_t, int, int,
                              void*) {
+  return QLIN_EINVAL;
+}
+extern "C" int qlin_quantize(const void*, int, int64_t, int64_t, int, int, int, const void*,
+                             const void*, void*, void*, void*, uint32_t*, uint32_t*, void*) {
   return QLIN_EINVAL;
 }
