@@ -143,11 +143,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    # BENCH_DIST_BACKEND=gloo + BENCH_SHARE_GPU=1: rehearse the N > 1 path with several ranks on
+    # one GPU (the driver's multi-GPU runs use RCCL, one rank per GPU)
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    gpu = local % torch.cuda.device_count() if os.environ.get("BENCH_SHARE_GPU") else local
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     M, N_full, K, bits, group, ring, kernel, note = WORKLOADS[args.workload]
     N = N_full
@@ -229,7 +235,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev_s = e0.elapsed_time(e1) / 1e3
-    t = torch.tensor([ev_s], dtype=torch.float64, device=dev)
+    t = torch.tensor([ev_s], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -251,7 +257,7 @@ def main():
                 "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
     roof["traffic"] = None
-    pmc = _pmc_traffic(args.workload)
+    pmc = _pmc_traffic(args.workload) if not (args.split and world > 1) else None
     if pmc is not None:
         roof["traffic"] = round(pmc["fetch_bytes_per_launch"])
         roof["traffic_source"] = pmc["file"]
