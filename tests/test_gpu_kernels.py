@@ -218,3 +218,15 @@ def test_gptq_checkpoint_conversion(bits, group):
     x = rand_x(3, K, seed=2)
     y = ql(t(x).unsqueeze(0))[0]
     assert_close_to_ref(n(y), O.linear_ref(x, ref_w, tensors["lin.bias"].numpy()))
+
+
+@pytest.mark.parametrize("bits,group", [(4, 128), (4, 64), (3, 64), (2, 32)])
+def test_gemm_wide_tile(bits, group):
+    """The 128 x 512 block tile (taken when the grid has >= 2 blocks per CU: the configs[2]
+    shape) with ragged M and N; g64 / g32 take its checked k-step form."""
+    M, N, K = 8192 + 33, 4096 + 16, 1024
+    qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=bits + group)
+    x = rand_x(M, K, seed=7)
+    y = n(qlin.gemm(t(x), qw, qsz, None, N, K, bits, group, fl))
+    rows = np.r_[0:64, M // 2 - 64:M // 2 + 64, M - 96:M]  # a sample of rows keeps the fp64 ref cheap
+    assert_close_to_ref(y[rows], O.linear_ref(x[rows], wdq), what=f"wide gemm b{bits} g{group}")
