@@ -67,8 +67,10 @@ struct XRaw {
 };
 
 struct Geo {
-  const uint32_t* qw_nt;  // this block's tile row of qweight (uniform)
-  const uint32_t* sz_nt;  // this block's row tile of qsz (uniform)
+  const uint32_t* qw_nt;  // this block's first tile row of qweight (uniform)
+  const uint32_t* sz_nt;  // this block's first row tile of qsz (uniform)
+  int64_t wstride, szstride;  // words between consecutive row tiles of qweight / qsz
+  int jmax;                   // last valid row tile of the block, relative to its first
   const _Float16* xrow;   // x row this lane loads (row min(lane / (64/MT), M-1))
   int K, G, group, lane, n_in, xk;  // xk: the lane's first k inside a tile
   uint32_t gmagic;                   // ceil(2^31 / (group / 32)): branch-free k / group
@@ -81,12 +83,15 @@ __device__ __forceinline__ int group_of(const Geo& g, int k) {
   return min(gi, g.G - 1);
 }
 
-template <int BITS, int GPT>
-__device__ __forceinline__ void load_w(WTile<BITS, GPT>& t, const Geo& g, int kt) {
-  t.pc = load_piece_nt<BITS>(g.qw_nt + kt * 64 * BITS + g.lane * BITS);
+// row tile j of the block (clamped to its last valid tile: those loads feed outputs never stored)
+template <int NTB, int BITS, int GPT>
+__device__ __forceinline__ void load_w(WTile<BITS, GPT>& t, const Geo& g, int kt, int j) {
+  const int jj = NTB == 1 ? 0 : min(j, g.jmax);
+  t.pc = load_piece_nt<BITS>(g.qw_nt + jj * g.wstride + kt * 64 * BITS + g.lane * BITS);
 #pragma unroll
   for (int i = 0; i < GPT; ++i)
-    t.sz[i] = g.sz_nt[group_of(g, kt * kTileK + 32 * (i * 4 / GPT)) * kTileN + g.n_in];
+    t.sz[i] = g.sz_nt[jj * g.szstride +
+                      group_of(g, kt * kTileK + 32 * (i * 4 / GPT)) * kTileN + g.n_in];
 }
 
 template <int MT>
@@ -149,14 +154,17 @@ __device__ __forceinline__ void park_x(h8 (&xa)[4], const XRaw<MT>& r, uint32_t*
   for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, b[4 * s]);
 }
 
-template <int BITS, int MT, int GPT, int ZM, int PF>
+// NTB row tiles per block share each parked x tile (x is re-read from L2 once per block, so
+// for M >= 8 a block of several row tiles cuts the x traffic that otherwise dominates)
+template <int BITS, int MT, int GPT, int ZM, int PF, int NTB>
 __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0, int nts,
-                                          int ktl, f4& acc, const ActQ& aq, float aq_sc,
+                                          int ktl, f4 (&acc)[NTB], const ActQ& aq, float aq_sc,
                                           float aq_zp) {
   const Magics mg = make_magics<BITS>();
 
   // FULL: the tile is not the matrix's last (only that one can hold fewer than 4 k-steps)
-  auto step = [&](const WTile<BITS, GPT>& t, const h8 (&xa)[4], int kt, auto S_, auto FULL_) {
+  auto step = [&](const WTile<BITS, GPT>& t, f4& ac, const h8 (&xa)[4], int kt, auto S_,
+                  auto FULL_) {
     constexpr int S = decltype(S_)::value;
     constexpr bool FULL = decltype(FULL_)::value;
     constexpr int slot = S * GPT / 4;
@@ -166,26 +174,30 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
       const GroupQ gq = make_group_w<BITS, ZM>(t.sz[slot]);
       dequant_step<BITS, ZM, S>(t.pc, mg, gq, v);
       const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, acc, 0, 0, 0);
+      ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, ac, 0, 0, 0);
     }
   };
-  auto tile = [&](const WTile<BITS, GPT>& t, XRaw<MT>& xr, int kt, auto FULL_) {
+  auto tile = [&](const WTile<BITS, GPT> (&t)[NTB], XRaw<MT>& xr, int kt, auto FULL_) {
     h8 xa[4];
     if (aq.on) fake_quant_x<MT>(xr, aq, aq_sc, aq_zp);  // wave-uniform
     park_x<MT>(xa, xr, xslot, g.lane, g.n_in);
-    step(t, xa, kt, std::integral_constant<int, 0>{}, FULL_);
-    step(t, xa, kt, std::integral_constant<int, 1>{}, FULL_);
-    step(t, xa, kt, std::integral_constant<int, 2>{}, FULL_);
-    step(t, xa, kt, std::integral_constant<int, 3>{}, FULL_);
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) {
+      step(t[j], acc[j], xa, kt, std::integral_constant<int, 0>{}, FULL_);
+      step(t[j], acc[j], xa, kt, std::integral_constant<int, 1>{}, FULL_);
+      step(t[j], acc[j], xa, kt, std::integral_constant<int, 2>{}, FULL_);
+      step(t[j], acc[j], xa, kt, std::integral_constant<int, 3>{}, FULL_);
+    }
   };
 
   // prologue: PF tiles (codes, (scale, zero), x) in flight, tile index clamped to the wave's last
-  WTile<BITS, GPT> wt[PF];
+  WTile<BITS, GPT> wt[PF][NTB];
   XRaw<MT> xq[PF];
 #pragma unroll
   for (int u = 0; u < PF; ++u) {
     load_x<MT>(xq[u], g, min(kt0 + u, ktl));
-    load_w(wt[u], g, min(kt0 + u, ktl));
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) load_w<NTB>(wt[u][j], g, min(kt0 + u, ktl), j);
   }
 
   // full rounds of PF tiles: compute tile t, refill its slot with tile t + PF
@@ -196,7 +208,8 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
       const int kt = kt0 + t0 + u;
       tile(wt[u], xq[u], kt, std::true_type{});
       load_x<MT>(xq[u], g, min(kt + PF, ktl));
-      load_w(wt[u], g, min(kt + PF, ktl));
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) load_w<NTB>(wt[u][j], g, min(kt + PF, ktl), j);
     }
   }
   // last round (1..PF tiles): compute only; a tile short of K (the matrix's last) takes the
@@ -212,19 +225,19 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
 
 }
 
-template <int BITS, int MT, int GPT, int ZM, int PF>
+template <int BITS, int MT, int GPT, int ZM, int PF, int NTB = 1>
 __global__ __launch_bounds__(1024) void gemv_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
     int M, int N, int K, int group, uint32_t gmagic, int tpw, const _Float16* __restrict__ res,
     int ep, ActQ aq) {
-  __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
+  __shared__ __attribute__((aligned(16))) float red[NTB * MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
   __shared__ float aq_s[2][MT];
   const int W = blockDim.x >> 6;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
-  const int nt = blockIdx.x;
+  const int nt = blockIdx.x * NTB;  // first row tile of the block
   const int Kt = (K + kTileK - 1) / kTileK;
   Geo g;
   g.K = K;
@@ -235,6 +248,9 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
   g.n_in = g.lane & 15;
   g.qw_nt = qw + (int64_t)nt * Kt * 64 * BITS;
   g.sz_nt = qsz + (int64_t)nt * g.G * kTileN;
+  g.wstride = (int64_t)Kt * 64 * BITS;
+  g.szstride = (int64_t)g.G * kTileN;
+  g.jmax = min(NTB, (N + kTileN - 1) / kTileN - nt) - 1;
   constexpr int LPR = 64 / MT;  // lanes per x row
   g.xrow = x + (int64_t)min(g.lane / LPR, M - 1) * K;
   g.xk = 2 * MT * (g.lane % LPR);
@@ -284,22 +300,29 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
     aq_zp = aq_s[1][r];
   }
 
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  gemv_body<BITS, MT, GPT, ZM, PF>(g, &xs[wave][0], kt0, nts, ktl, acc, aq, aq_sc, aq_zp);
+  f4 acc[NTB];
+#pragma unroll
+  for (int j = 0; j < NTB; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+  gemv_body<BITS, MT, GPT, ZM, PF, NTB>(g, &xs[wave][0], kt0, nts, ktl, acc, aq, aq_sc, aq_zp);
 
   // combine the W partials of each (row m < MT, column n): C row m = 4q + i sits in lane
   // n + 16q, element i; layout [m][n][wave] so one thread reads its 16 partials with 4
   // ds_read_b128
+  // (row tile j of the block: [j][m][n][wave])
   const int q4 = 4 * (g.lane >> 4);
   if (q4 < MT) {
 #pragma unroll
-    for (int i = 0; i < 4 && i < MT; ++i)
-      red[((q4 + i) * kTileN + g.n_in) * kMaxWaves + wave] = acc[i];
-    if (wave == 0) {
-      for (int w = W; w < kMaxWaves; ++w)
+    for (int j = 0; j < NTB; ++j) {
+      float* rj = red + j * MT * kTileN * kMaxWaves;
 #pragma unroll
-        for (int i = 0; i < 4 && i < MT; ++i)
-          red[((q4 + i) * kTileN + g.n_in) * kMaxWaves + w] = 0.f;
+      for (int i = 0; i < 4 && i < MT; ++i)
+        rj[((q4 + i) * kTileN + g.n_in) * kMaxWaves + wave] = acc[j][i];
+      if (wave == 0) {
+        for (int w = W; w < kMaxWaves; ++w)
+#pragma unroll
+          for (int i = 0; i < 4 && i < MT; ++i)
+            rj[((q4 + i) * kTileN + g.n_in) * kMaxWaves + w] = 0.f;
+      }
     }
   }
   __syncthreads();
@@ -313,19 +336,23 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
     return (float)(_Float16)t;  // F.linear's fp16 output
   };
   if (ep == kEpSiluMul) {  // N even, interleaved halves: 8 outputs per tile and row m
-    for (int o = tid; o < MT * 8; o += blockDim.x) {
-      const int m = o >> 3, n = o & 7;
-      const int64_t row = (int64_t)nt * kTileN + n;
+    for (int o = tid; o < NTB * MT * 8; o += blockDim.x) {
+      const int j = o / (MT * 8), oo = o - j * MT * 8;
+      const int m = oo >> 3, n = oo & 7;
+      const int64_t ntj = (int64_t)nt + j;
+      const int64_t row = ntj * kTileN + n;
+      const int b = j * MT * kTileN;
       if (m < M && row + 8 < N) {
-        const float g = total(m * kTileN + n, row), u = total(m * kTileN + n + 8, row + 8);
-        y[(int64_t)m * (N >> 1) + nt * 8 + n] = (_Float16)(silu_rn16(g) * u);
+        const float g = total(b + m * kTileN + n, row), u = total(b + m * kTileN + n + 8, row + 8);
+        y[(int64_t)m * (N >> 1) + ntj * 8 + n] = (_Float16)(silu_rn16(g) * u);
       }
     }
     return;
   }
-  for (int o = tid; o < MT * kTileN; o += blockDim.x) {
-    const int m = o / kTileN, n = o - m * kTileN;
-    const int64_t row = (int64_t)nt * kTileN + n;
+  for (int o = tid; o < NTB * MT * kTileN; o += blockDim.x) {
+    const int j = o / (MT * kTileN), oo = o - j * MT * kTileN;
+    const int m = oo / kTileN, n = oo - m * kTileN;
+    const int64_t row = ((int64_t)nt + j) * kTileN + n;
     if (m < M && row < N) {
       float t = total(o, row);
       if (ep == kEpResidual) t += (float)res[(int64_t)m * N + row];
@@ -394,18 +421,24 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st, const Ep& e) {
   const int Nt = (N + kTileN - 1) / kTileN;
   const int Kt = (K + kTileK - 1) / kTileK;
+  // 8-16 token rows on a wide matrix: two row tiles per block share each parked x tile (x is
+  // re-read from L2 per block); measured (tools/dev/gemv_geo.py) 14336 x 4096, M = 16: 24.5 ->
+  // 15.7 us, M = 8: 12.0 -> 10.2 us; no gain at N = 4096 and for M <= 4, so those keep one
+  const int ntb = (MT >= 8 && Nt >= 512) ? 2 : 1;
+  const int blocks = (Nt + ntb - 1) / ntb;
   int tpw = 0;
-  const int W = pick_waves(Nt, Kt, tpw);
+  const int W = pick_waves(blocks, Kt, tpw);
   const uint32_t gs = group_magic(group);
-#define QLIN_GV(PF)                                                                        \
-  hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, ZM, PF>), dim3(Nt), dim3(64 * W), \
+#define QLIN_GV(PF, T)                                                                     \
+  hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, ZM, PF, T>), dim3(blocks), dim3(64 * W), \
                      0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias,             \
                      (_Float16*)y, M, N, K, group, gs, tpw, (const _Float16*)e.res, e.ep, e.aq)
   if constexpr (MT >= 8) {  // x registers of 4 tiles in flight would spill
-    QLIN_GV(2);
+    if (ntb == 2) QLIN_GV(2, 2);
+    else QLIN_GV(2, 1);
   } else {
-    if (tpw <= 2) QLIN_GV(2);
-    else QLIN_GV(4);
+    if (tpw <= 2) QLIN_GV(2, 1);
+    else QLIN_GV(4, 1);
   }
 #undef QLIN_GV
   return (int)hipGetLastError();
