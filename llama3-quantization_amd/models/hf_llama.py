@@ -1,4 +1,4 @@
-"""Local Hugging Face LLaMA checkpoints and wikitext2 text -> the quantized evaluation model
+"""Local Hugging Face LLaMA / OPT checkpoints and wikitext2 text -> the quantized evaluation model
 (the reference's main.py path: LMClass loads the model (models/LMClass.py:26-45), omniquant()
 wraps every decoder layer in QuantLlamaDecoderLayer and RTN-quantizes it (quant/omniquant.py:
 195-314 with epochs = 0), evaluate() runs the wikitext2 perplexity loop (main.py:102-154) on
@@ -14,13 +14,17 @@ import os
 import numpy as np
 import torch
 
+from torch import nn
+
 from quant.omni_norm import OmniLlamaRMSNorm
 from .int_llama_layer import QuantLlamaDecoderLayer
-from .quant_llama import QuantLlamaForEval
+from .int_opt_layer import QuantOPTDecoderLayer
+from .quant_llama import QuantLlamaForEval, causal_mask
 
 
 def load_hf_llama(path: str, dtype=torch.float16, device="cpu"):
-    """LlamaForCausalLM from a local directory (models/LMClass.py:39-41 loads it in fp16)."""
+    """LlamaForCausalLM / OPTForCausalLM from a local directory (models/LMClass.py:39-41 loads it
+    in fp16)."""
     from transformers import AutoModelForCausalLM
     model = AutoModelForCausalLM.from_pretrained(path, torch_dtype=dtype, local_files_only=True)
     return model.to(device).eval()
@@ -37,6 +41,53 @@ def quant_llama_from_hf(model, args):
     q = QuantLlamaForEval(cfg, layers, model.model.embed_tokens, norm, model.lm_head)
     q.layer_ids = list(range(len(layers)))
     return q
+
+
+class QuantOPTForEval(nn.Module):
+    """OPTForCausalLM's decoder with the reference's QuantOPTDecoderLayer in place of HF's
+    (BASELINE configs[0]: OPT-125M): token + learned position embeddings (offset 2, no padding),
+    optional project_in / project_out, the causal additive mask, final LayerNorm, lm_head."""
+
+    def __init__(self, config, hf_decoder, layers, lm_head):
+        super().__init__()
+        self.config = config
+        self.embed_tokens = hf_decoder.embed_tokens
+        self.embed_positions = hf_decoder.embed_positions
+        self.project_in = getattr(hf_decoder, "project_in", None)
+        self.project_out = getattr(hf_decoder, "project_out", None)
+        self.final_layer_norm = getattr(hf_decoder, "final_layer_norm", None)
+        self.layers = nn.ModuleList(layers)
+        self.lm_head = lm_head
+
+    def forward(self, input_ids):
+        bsz, T = input_ids.shape
+        h = self.embed_tokens(input_ids)
+        if self.project_in is not None:
+            h = self.project_in(h)
+        pos = torch.arange(T, device=input_ids.device) + getattr(self.embed_positions, "offset", 2)
+        h = h + self.embed_positions.weight[pos][None].to(h.dtype)
+        mask = causal_mask(bsz, T, h.dtype, h.device)
+        for layer in self.layers:
+            h = layer(h, attention_mask=mask)[0]
+        if self.final_layer_norm is not None:
+            h = self.final_layer_norm(h)
+        if self.project_out is not None:
+            h = self.project_out(h)
+        return self.lm_head(h)
+
+
+@torch.no_grad()
+def quant_model_from_hf(model, args):
+    """LLaMA or OPT (config.model_type) -> the quantized evaluation model."""
+    if model.config.model_type == "opt":
+        layers = [QuantOPTDecoderLayer(model.config, layer, args)
+                  for layer in model.model.decoder.layers]
+        q = QuantOPTForEval(model.config, model.model.decoder, layers, model.lm_head)
+        q.layer_ids = list(range(len(layers)))
+        return q
+    if model.config.model_type == "llama":
+        return quant_llama_from_hf(model, args)
+    raise NotImplementedError(f"model_type {model.config.model_type!r} (LLaMA and OPT only)")
 
 
 def wikitext2_test_ids(source: str, tokenizer=None) -> torch.Tensor:

@@ -80,3 +80,41 @@ def test_eval_ppl_tool_quantized_modes(tmp_path):
     assert np.isfinite(res["fake"])
     for mode in ("packed", "fused"):
         assert abs(res[mode] - res["fake"]) / res["fake"] < 1e-3, res
+
+
+def _tiny_opt(path, dtype=torch.float32):
+    from transformers import OPTConfig, OPTForCausalLM
+    cfg = OPTConfig(hidden_size=128, ffn_dim=512, num_attention_heads=4, num_hidden_layers=2,
+                    vocab_size=512, max_position_embeddings=512, word_embed_proj_dim=128)
+    torch.manual_seed(0)
+    m = OPTForCausalLM(cfg).to(dtype).eval()
+    m.save_pretrained(path)
+    return m
+
+
+def test_opt_conversion_matches_hf_forward(tmp_path):
+    """BASELINE configs[0]'s model family: OPTForCausalLM -> QuantOPTDecoderLayer stack."""
+    from models.hf_llama import load_hf_llama, quant_model_from_hf
+    from models.quant_llama import quant_args
+    _tiny_opt(tmp_path / "opt")
+    hf = load_hf_llama(str(tmp_path / "opt"), torch.float32, "cpu")
+    q = quant_model_from_hf(hf, quant_args(16, 128))
+    ids = torch.from_numpy(np.random.RandomState(3).randint(0, 512, size=(1, 33)))
+    with torch.no_grad():
+        ref = hf(ids).logits
+        got = q(ids)
+    rel = ((got - ref).abs().max() / ref.abs().max()).item()
+    assert rel < 1e-4, rel
+
+
+@pytest.mark.gpu
+def test_opt_int8_per_channel_packed_vs_fake(tmp_path):
+    """BASELINE configs[0]: OPT int8 per-channel weights (biased linears), fake-quant vs packed."""
+    import eval_ppl
+    _tiny_opt(tmp_path / "opt", torch.float16)
+    _tokens(tmp_path / "ids.npy", n=2 * 256)
+    res = {mode: eval_ppl.run(eval_ppl.parse(["--model", str(tmp_path / "opt"), "--data",
+                                              str(tmp_path / "ids.npy"), "--wbits", "8",
+                                              "--group", "0", "--seqlen", "256", "--mode",
+                                              mode]))["ppl"] for mode in ("fake", "packed")}
+    assert np.isfinite(res["fake"]) and abs(res["packed"] - res["fake"]) / res["fake"] < 1e-3, res

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Wikitext2 perplexity of a local LLaMA checkpoint, RTN-quantized as the reference's main.py
+"""Wikitext2 perplexity of a local LLaMA (or OPT) checkpoint, RTN-quantized as the reference's main.py
 does (``--wbits 4 --group_size 128 --epochs 0 [--real_quant]``), on one MI355X:
 
   python tools/eval_ppl.py --model /path/to/Meta-Llama-3-8B --data /path/to/wikitext2_test \\
@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "llama3-quantization_amd"))
 
 import torch  # noqa: E402
 
-from models.hf_llama import load_hf_llama, quant_llama_from_hf, wikitext2_test_ids  # noqa: E402
+from models.hf_llama import load_hf_llama, quant_model_from_hf, wikitext2_test_ids  # noqa: E402
 from models.quant_llama import nll_from_logits, quant_args, rtn_quantize_  # noqa: E402
 from quant.utils import pack_quant_linears  # noqa: E402
 
@@ -37,12 +37,13 @@ def run(a):
         from transformers import AutoTokenizer
         tok = AutoTokenizer.from_pretrained(a.model, local_files_only=True)
     ids = wikitext2_test_ids(a.data, tok)
-    q = quant_llama_from_hf(model, quant_args(a.wbits, a.group, a.abits))
+    q = quant_model_from_hf(model, quant_args(a.wbits, a.group or None, a.abits))
     if a.wbits < 16:
         rtn_quantize_(q, pack=a.mode in ("packed", "fused"))
         if a.mode == "fused":
             for layer in q.layers:
-                layer.fuse_packed_projections()
+                if hasattr(layer, "fuse_packed_projections"):  # LLaMA layers
+                    layer.fuse_packed_projections()
     seqlen = a.seqlen
     nsamples = ids.numel() // seqlen
     nlls, ms = [], []
@@ -70,7 +71,7 @@ def parse(argv=None):
     ap.add_argument("--model", required=True)
     ap.add_argument("--data", required=True)
     ap.add_argument("--wbits", type=int, default=4)
-    ap.add_argument("--group", type=int, default=128)
+    ap.add_argument("--group", type=int, default=128, help="0: per-channel (no groups)")
     ap.add_argument("--abits", type=int, default=16)
     ap.add_argument("--seqlen", type=int, default=2048)
     ap.add_argument("--mode", choices=("fake", "packed", "fused"), default="packed")
