@@ -126,7 +126,17 @@ def cpu_baseline(M, N, K, bits, group, seconds):
         reps += 1
     quant_ms = (time.perf_counter() - t1) / reps * 1e3
     del y
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     return {"value": round(tflops, 6), "unit": "TFLOP/s", "cores": int(threads), "kind": "port",
+            "cpu_model": cpu_model, "nproc": os.cpu_count(),
             "sample": (f"oracle (numpy fp32 BLAS) x@W_dq^T, M={M} N={N} K={K}, {nmat} distinct "
                        f"pre-dequantized int{bits} g{group} matrices cycled for {dt:.1f}s "
                        f"({launches} products; reference eval mode ii)"),
