@@ -154,9 +154,9 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
  * act_bits != 0 additionally fake-quantizes x per token first — QuantLinear.forward's
  * act_quantizer(input) (quant/int_linear.py:59-60) with UniformAffineQuantizer(n_bits=act_bits,
  * dynamic_method="per_token") (quant/quantizer.py:132-159, :94-115), bit-exact; act_flags takes
- * QLIN_SYMMETRIC / QLIN_DISABLE_ZERO_POINT.  M <= 64: fused into the GEMV (each block recomputes
- * the token's min / max; x 16-byte aligned, K % 8 == 0); M > 64: the quantizer kernel writes
- * x_dq to `workspace` (fp16 [M, K], required) before the GEMM.
+ * QLIN_SYMMETRIC / QLIN_DISABLE_ZERO_POINT.  M <= 64 and N <= 16384: fused into the GEMV (each
+ * block recomputes the token's min / max; x 16-byte aligned, K % 8 == 0); otherwise the quantizer
+ * kernel writes x_dq to `workspace` (fp16 [M, K], required then) before the GEMV / GEMM.
  * Same kernels and dispatch as qlin_linear_f16 (GEMV for M <= 64, MFMA GEMM above).
  */
 #define QLIN_EP_NONE     0

@@ -35,6 +35,7 @@ namespace {
 constexpr int kWaves = 8;
 constexpr int BM = 128, BK = kTileK;  // block rows; one packed k-tile per stage
 constexpr int64_t kSkinnyMaxM = 64;   // qlin_linear_f16: M <= this runs the GEMV kernel
+constexpr int64_t kActFuseMaxN = 16384;  // act fake-quant fused into the GEMV up to this N
 
 typedef __attribute__((address_space(3))) void* lds_ptr;
 typedef __attribute__((address_space(1))) void* gbl_ptr;
@@ -412,6 +413,19 @@ extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, 
   if (M < 0) return QLIN_EINVAL;
   if (M == 0) return QLIN_OK;
   const int64_t ny = epilogue == kEpSiluMul ? N / 2 : N;  // columns of y (and residual)
+  // the fused activation statistics are recomputed by every GEMV block: past ~1024 row tiles
+  // the quantizer launch + plain GEMV is cheaper (tools/dev/act_ab.py: 28672 x 4096 fused
+  // 24.0 us vs 22.6 us; 4096 x 4096 fused 7.0 us vs 12.8 us)
+  const bool fuse_act = act_bits && M <= kSkinnyMaxM && N <= kActFuseMaxN;
+  if (act_bits && !fuse_act) {
+    if (!workspace) return QLIN_EINVAL;
+    const int rc = qlin_quantize(x, QLIN_F16, M, K, act_bits, (int)K,
+                                 act_flags & (QLIN_SYMMETRIC | QLIN_DISABLE_ZERO_POINT), nullptr,
+                                 nullptr, workspace, nullptr, nullptr, nullptr, nullptr, stream);
+    if (rc) return rc;
+    x = workspace;
+    act_bits = 0;
+  }
   if (M <= kSkinnyMaxM) {
     for (int64_t m0 = 0; m0 < M; m0 += 16) {
       const int64_t mc = M - m0 < 16 ? M - m0 : 16;
@@ -421,14 +435,6 @@ extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, 
       if (rc) return rc;
     }
     return QLIN_OK;
-  }
-  if (act_bits) {  // batched tokens: the quantizer kernel writes x_dq into the workspace first
-    if (!workspace) return QLIN_EINVAL;
-    const int rc = qlin_quantize(x, QLIN_F16, M, K, act_bits, (int)K,
-                                 act_flags & (QLIN_SYMMETRIC | QLIN_DISABLE_ZERO_POINT), nullptr,
-                                 nullptr, workspace, nullptr, nullptr, nullptr, nullptr, stream);
-    if (rc) return rc;
-    x = workspace;
   }
   return gemm_ep(qweight, qsz, flags, x, bias, residual, y, M, N, K, bits, group, epilogue,
                  stream);

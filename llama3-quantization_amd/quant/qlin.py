@@ -297,6 +297,7 @@ def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0):
 
 
 SKINNY_MAX_M = 64  # qlin_linear_*: M <= this runs the GEMV kernel
+ACT_FUSE_MAX_N = 16384  # qlin_linear_ep_f16 fuses the act fake-quant into the GEMV up to this N
 EP_NONE = 0
 EP_RESIDUAL = 1
 EP_SILU_MUL = 2
@@ -327,7 +328,7 @@ def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NON
     if M == 0:
         return y
     ws = None
-    if act_bits and M > SKINNY_MAX_M:
+    if act_bits and (M > SKINNY_MAX_M or N > ACT_FUSE_MAX_N):
         ws = torch.empty(M, K, dtype=torch.float16, device=x.device)
     rc = load_library().qlin_linear_ep_f16(_ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(bias),
                                            _ptr(residual), _ptr(y), M, N, K, bits, group,

@@ -115,7 +115,7 @@ def test_fused_act_quant_matches_two_launches(M, abits, aflags):
     or run by the quantizer kernel into the workspace (M > 64) — bit-identical to the reference
     order act_quantizer(x) (quantizer kernel, itself bit-exact with the reference) then the
     packed linear."""
-    N, K = 272, 1024
+    N, K = (272, 1024) if M != 2 else (16400, 256)  # N > 16384: the quantizer + GEMV leg
     qw, qsz, fl = _packed(N, K, 11)
     x = t((np.random.RandomState(M + abits).randn(M, K) * 2).astype(np.float16))
     xdq = qlin.quantize(x, abits, K, aflags, want_params=False)["x_dq"]
