@@ -121,15 +121,10 @@ __global__ __launch_bounds__(kThreads) void quantize_kernel(
   }
   __syncthreads();
 
-  // phase 2: one group per thread
+  // phase 2: per group, min / max over its chunks, then the calibration
   const int ngr = nch / P.cpg;
   const int64_t g0 = row0 * (P.K / P.group);
-  for (int gi = tid; gi < ngr; gi += kThreads) {
-    float mn = s_min[gi * P.cpg], mx = s_max[gi * P.cpg];
-    for (int j = 1; j < P.cpg; ++j) {
-      mn = min_nan(mn, s_min[gi * P.cpg + j]);
-      mx = max_nan(mx, s_max[gi * P.cpg + j]);
-    }
+  auto finish_group = [&](int gi, float mn, float mx) {
     float upf = 1.f, lowf = 1.f;
     if (P.flags & QLIN_LWC) { upf = (float)up[g0 + gi]; lowf = (float)low[g0 + gi]; }
     float scale, zp;
@@ -144,6 +139,31 @@ __global__ __launch_bounds__(kThreads) void quantize_kernel(
       const int g = gi - (gi / Gr) * Gr;
       qsz[sz_index(row >> 4, g, Gr, (int)(row & 15))] =
           sz_pack((_Float16)scale, has_zp ? (int)zp : (1 << (BITS - 1)));
+    }
+  };
+  if (P.cpg <= 8) {  // small groups (g <= 256): one group per thread
+    for (int gi = tid; gi < ngr; gi += kThreads) {
+      float mn = s_min[gi * P.cpg], mx = s_max[gi * P.cpg];
+      for (int j = 1; j < P.cpg; ++j) {
+        mn = min_nan(mn, s_min[gi * P.cpg + j]);
+        mx = max_nan(mx, s_max[gi * P.cpg + j]);
+      }
+      finish_group(gi, mn, mx);
+    }
+  } else {  // long groups (per-channel weights, per-token activations): one group per wave
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int gi = wave; gi < ngr; gi += kThreads / 64) {
+      float mn = __builtin_inff(), mx = -__builtin_inff();
+      for (int j = lane; j < P.cpg; j += 64) {
+        mn = min_nan(mn, s_min[gi * P.cpg + j]);
+        mx = max_nan(mx, s_max[gi * P.cpg + j]);
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        mn = min_nan(mn, __shfl_xor(mn, o));
+        mx = max_nan(mx, __shfl_xor(mx, o));
+      }
+      if (lane == 0) finish_group(gi, mn, mx);
     }
   }
   __syncthreads();
