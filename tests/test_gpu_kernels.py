@@ -230,3 +230,23 @@ def test_gemm_wide_tile(bits, group):
     y = n(qlin.gemm(t(x), qw, qsz, None, N, K, bits, group, fl))
     rows = np.r_[0:64, M // 2 - 64:M // 2 + 64, M - 96:M]  # a sample of rows keeps the fp64 ref cheap
     assert_close_to_ref(y[rows], O.linear_ref(x[rows], wdq), what=f"wide gemm b{bits} g{group}")
+
+
+@pytest.mark.parametrize("N", [8192 + 16 * 3 + 5, 8192 + 16])
+def test_gemv_two_row_tiles_per_block(N):
+    """8-16 token rows on a wide matrix take two row tiles per block (odd tile counts clamp the
+    last block's second tile)."""
+    K, group = 512, 128
+    qw, qsz, fl, wdq = _packed(N, K, 4, group, seed=N)
+    bias = np.random.RandomState(5).randn(N).astype(np.float16) * np.float16(0.1)
+    for M in (5, 8, 13, 16):
+        x = rand_x(M, K, seed=M)
+        y = qlin.gemv(t(x), qw, qsz, t(bias), N, K, 4, group, fl)
+        assert_close_to_ref(n(y), O.linear_ref(x, wdq, bias), what=f"gemv ntb2 M{M} N{N}")
+    if N % 16 == 0:  # the residual epilogue on the same path
+        x = rand_x(16, K, seed=3)
+        r = rand_x(16, N, seed=4)
+        got = qlin.linear_ep(t(x), qw, qsz, None, N, K, 4, group, fl, epilogue=qlin.EP_RESIDUAL,
+                             residual=t(r))
+        ref = t(r) + qlin.gemv(t(x), qw, qsz, None, N, K, 4, group, fl)
+        assert torch.equal(got, ref)
