@@ -212,6 +212,19 @@ int qlin_rope_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k, in
                   const int64_t* position_ids, int64_t pos_batch_stride, float* q_out, uint16_t* k_out, int64_t B, int64_t S,
                   int Hq, int Hkv, int D, void* stream);
 
+/*
+ * Attention scores of a prefill window, in place (models/int_llama_layer.py:143-157 of the
+ * reference: attn_weights / sqrt(head_dim) + attention_mask, then torch.max(w, finfo(fp32).min)):
+ * one pass instead of three, bit-exact (torch divides an fp32 tensor by a scalar as a
+ * multiplication by the fp32 reciprocal).
+ *   scores fp32 [B, H, T, L] contiguous, L % 4 == 0;  mask [B', 1, T, L] additive, QLIN_F16 or
+ *   QLIN_F32, batch b at mask + b * mask_batch_stride elements (0: broadcast), or NULL (then only
+ *   the division, as the reference applies the clamp only with a mask).
+ */
+int qlin_attn_scores_f32(float* scores, const void* mask, int mask_dtype, int64_t B, int64_t H,
+                         int64_t T, int64_t L, int64_t mask_batch_stride, float scale_div,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,11 +13,16 @@
 // and apply_rotary_pos_emb (index by position_ids, q*cos + rotate_half(q)*sin in fp32 for q,
 // the same in fp16 for k: every product and the sum rounded to fp16 as torch's fp16 ops do).
 // Elementwise with the reference's op order and roundings: bit-exact.
+//
+// qlin_attn_scores_f32 replaces, for prefill windows, the three fp32 passes over the
+// [B, H, T, L] score tensor after QK^T (models/int_llama_layer.py:143-157: / sqrt(head_dim),
+// + attention_mask, torch.max(w, finfo.min)) with one in-place pass, bit-exact.
 #include "qlin_common.h"
 #include "../../include/qlin_gfx950.h"
 
 namespace {
 
+using qlin::h2;
 using qlin::h8;
 
 constexpr int kNormThreads = 256;
@@ -132,7 +137,69 @@ __global__ __launch_bounds__(256) void rope_kernel(
   }
 }
 
+// attention scores of a prefill window, in place: w = max(w / scale + mask, finfo(fp32).min)
+// (w / scale alone without a mask)
+// with torch's scalar division (multiplication by the fp32 reciprocal), one pass instead of three
+template <bool MASK32>
+__global__ __launch_bounds__(256) void attn_scores_kernel(float* __restrict__ w,
+                                                          const void* __restrict__ mask,
+                                                          int64_t n4, int64_t L, int64_t rows_per_b,
+                                                          int64_t T, int64_t mask_bs, float inv) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int64_t e = 4 * i;             // L % 4 == 0: the four elements share a row
+  const int64_t row = e / L, l = e - row * L;
+  const int64_t b = row / rows_per_b;  // rows_per_b = H * T
+  const int64_t t = row % T;
+  float4 v = reinterpret_cast<float4*>(w)[i];
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
+  if (mask) {
+    const int64_t mo = b * mask_bs + t * L + l;
+    if constexpr (MASK32) {
+      const float4 mm = *reinterpret_cast<const float4*>((const float*)mask + mo);
+      m[0] = mm.x; m[1] = mm.y; m[2] = mm.z; m[3] = mm.w;
+    } else {
+      const uint2 mm = *reinterpret_cast<const uint2*>((const _Float16*)mask + mo);
+      const h2 a = __builtin_bit_cast(h2, mm.x), c = __builtin_bit_cast(h2, mm.y);
+      m[0] = (float)a.x; m[1] = (float)a.y; m[2] = (float)c.x; m[3] = (float)c.y;
+    }
+  }
+  float* vv = reinterpret_cast<float*>(&v);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float s = vv[j] * inv;
+    if (mask) {  // the reference clamps only after adding a mask
+      s = s + m[j];
+      s = (s != s) ? s : fmaxf(s, -3.402823466e38f);  // torch.max(w, finfo.min): NaN stays
+    }
+    vv[j] = s;
+  }
+  reinterpret_cast<float4*>(w)[i] = v;
+}
+
 }  // namespace
+
+extern "C" int qlin_attn_scores_f32(float* scores, const void* mask, int mask_dtype, int64_t B,
+                                    int64_t H, int64_t T, int64_t L, int64_t mask_batch_stride,
+                                    float scale_div, void* stream) {
+  if (!scores || B < 0 || H < 0 || T < 0 || L <= 0 || L % 4 || mask_batch_stride < 0 ||
+      (mask && mask_dtype != QLIN_F16 && mask_dtype != QLIN_F32) || !(scale_div > 0.f) ||
+      ((uintptr_t)scores & 15))
+    return QLIN_EINVAL;
+  const int64_t n4 = B * H * T * L / 4;
+  if (n4 == 0) return QLIN_OK;
+  if ((n4 + 255) / 256 > 0x7fffffff) return QLIN_EINVAL;
+  const float inv = 1.0f / scale_div;
+  const dim3 grid((unsigned)((n4 + 255) / 256));
+  if (mask_dtype == QLIN_F32)
+    hipLaunchKernelGGL(attn_scores_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, scores,
+                       mask, n4, L, H * T, T, mask_batch_stride, inv);
+  else
+    hipLaunchKernelGGL(attn_scores_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, scores,
+                       mask, n4, L, H * T, T, mask_batch_stride, inv);
+  return (int)hipGetLastError();
+}
 
 extern "C" int qlin_rmsnorm_f16(const uint16_t* x, const float* weight, uint16_t* y, int64_t rows,
                                 int64_t H, float eps, void* stream) {

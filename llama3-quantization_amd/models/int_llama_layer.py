@@ -264,16 +264,24 @@ class QuantLlamaAttention(nn.Module):
 
         query_states = self.qkt_matmul.quant_x1(query_states)
         key_states = self.qkt_matmul.quant_x2(key_states)
-        attn_weights = self.qkt_matmul(query_states, key_states.to(query_states.dtype).transpose(2, 3)) / math.sqrt(self.head_dim)
+        attn_weights = self.qkt_matmul(query_states, key_states.to(query_states.dtype).transpose(2, 3))
 
         if attn_weights.size() != (bsz, self.num_heads, q_len, kv_seq_len):
             raise ValueError(
                 f"Attention weights should be of size {(bsz, self.num_heads, q_len, kv_seq_len)}, but is"
                 f" {attn_weights.size()}")
-        if attention_mask is not None:
-            if attention_mask.size() != (bsz, 1, q_len, kv_seq_len):
-                raise ValueError(
-                    f"Attention mask should be of size {(bsz, 1, q_len, kv_seq_len)}, but is {attention_mask.size()}")
+        if attention_mask is not None and attention_mask.size() != (bsz, 1, q_len, kv_seq_len):
+            raise ValueError(
+                f"Attention mask should be of size {(bsz, 1, q_len, kv_seq_len)}, but is {attention_mask.size()}")
+        fused_scores = (self.rope_kernel and attn_weights.is_cuda
+                        and attn_weights.dtype == torch.float32
+                        and attn_weights.is_contiguous() and kv_seq_len % 4 == 0)
+        if fused_scores:
+            # fused mode: / sqrt(d), + mask, clamp as one in-place pass (bit-exact)
+            attn_weights = qlin.attn_scores_(attn_weights, attention_mask, math.sqrt(self.head_dim))
+        else:
+            attn_weights = attn_weights / math.sqrt(self.head_dim)
+        if attention_mask is not None and not fused_scores:
             attn_weights = attn_weights + attention_mask
             # == torch.max(w, torch.tensor(finfo.min)) of the reference (:155-157), without the
             # host->device scalar copy (keeps the layer capturable in a HIP graph)

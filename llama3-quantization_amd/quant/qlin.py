@@ -50,6 +50,7 @@ SIGNATURES = {
                            _i),
     "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),
     "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
+    "qlin_attn_scores_f32": ([_p, _p, _i, _l, _l, _l, _l, _l, ctypes.c_float, _p], _i),
     "qlin_attn_decode_partials_bytes": ([_l, _i, _i, _l], _l),
     "qlin_attn_decode": ([_p, _p, _p, _p, _p, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p], _i),
 }
@@ -412,6 +413,31 @@ def rope(q, k, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim
                                       B, S, n_heads, n_kv_heads, head_dim, _stream(q))
     _check(rc, "qlin_rope_f16")
     return q_out, k_out
+
+
+def attn_scores_(w, mask, scale_div):
+    """In place: w = max(w / scale_div + mask, finfo(fp32).min) (``qlin_attn_scores_f32``); w fp32
+    [B, H, T, L] contiguous, mask [B or 1, 1, T, L] fp16/fp32 or None.  Returns w."""
+    _dev(w)
+    if w.dtype != torch.float32 or w.dim() != 4 or w.shape[-1] % 4:
+        raise ValueError("scores must be contiguous fp32 [B, H, T, L] with L % 4 == 0")
+    B, H, T, L = w.shape
+    m, mbs, mdt = None, 0, F16
+    if mask is not None:
+        if mask.dtype not in (torch.float16, torch.float32) or mask.shape[-2:] != (T, L) or \
+                mask.shape[1] != 1 or mask.shape[0] not in (1, B):
+            raise ValueError(f"mask {tuple(mask.shape)} does not match scores {tuple(w.shape)}")
+        if mask.stride(-1) != 1 or mask.stride(-2) != L:
+            mask = mask.contiguous()
+        m = mask
+        mbs = mask.stride(0) if mask.shape[0] > 1 else 0
+        mdt = _DT[mask.dtype]
+        if not m.is_cuda:
+            raise RuntimeError("qlin kernels run on gfx950 only: got a CPU tensor")
+    rc = load_library().qlin_attn_scores_f32(_ptr(w), _ptr(m), mdt, B, H, T, L, mbs,
+                                             float(scale_div), _stream(w))
+    _check(rc, "qlin_attn_scores_f32")
+    return w
 
 
 ATTN_MAX_L = 4096

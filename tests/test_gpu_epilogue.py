@@ -144,3 +144,26 @@ def test_quantlinear_act_quant_fused_path(golden):
     ref = qlin.linear(t(g["x_dq"]).reshape(-1, K), ql.qweight, ql.qsz, None, 64, K, 4, ql.group,
                       ql.qflags).reshape(got.shape)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("mask", ["f16", "f32", "none", "bcast"])
+def test_attn_scores_pass_bit_exact(mask):
+    """/ sqrt(d) + mask + torch.max(w, finfo.min) in one in-place pass == the reference's three
+    torch ops (models/int_llama_layer.py:143-157)."""
+    import math
+    B, H, T, L = 2, 4, 37, 40
+    w = torch.randn(B, H, T, L, device="cuda") * 50
+    w[0, 0, 0, :3] = torch.tensor([float("nan"), float("-inf"), -3e38])
+    m = None
+    if mask != "none":
+        mm = torch.full((T, L), torch.finfo(torch.float16).min).triu(1 + L - T)
+        m = mm[None, None].expand(B if mask != "bcast" else 1, 1, T, L).contiguous()
+        m = m.to("cuda", torch.float16 if mask == "f16" else torch.float32)
+        if mask == "bcast":
+            m = m.expand(B, 1, T, L)
+    ref = w / math.sqrt(128)
+    if m is not None:
+        ref = (ref + m).clamp_min(torch.finfo(torch.float32).min)
+    got = qlin.attn_scores_(w.clone(), m, math.sqrt(128))
+    assert torch.equal(torch.nan_to_num(got, nan=7.0), torch.nan_to_num(ref, nan=7.0))
+    assert torch.isnan(got[0, 0, 0, 0])
