@@ -173,7 +173,8 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
  * / sqrt(head_dim), + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV bmm) on an fp16 K/V
  * cache; fp32 arithmetic, equal to the reference up to fp32 summation order.
  *   q    fp32 [B, Hq, D] (after RoPE);  k, v  fp16 [B, Hkv, L, D];  mask  fp16 [B, L] additive or
- *   NULL;  out  fp32 [B, Hq, D];  scale_div = sqrt(D) (the reference divides the scores by it).
+ *   NULL;  out  [B, Hq, D] in out_dtype: QLIN_F32, or QLIN_F16 = the fp32 result rounded once
+ *   (the layer's .to(fp16) before o_proj);  scale_div = sqrt(D) (the scores are divided by it).
  *   D == 128, Hq / Hkv in {1, 2, 4, 8}, L <= 4096.
  * The cache is split over blocks along L.  qlin_attn_decode_partials_bytes() returns the bytes
  * of `partials` scratch a call needs (0: none, pass NULL; -1: unsupported shapes); `counters` is
@@ -183,8 +184,8 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
  */
 int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L);
 int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
-                     float* out, int64_t B, int Hq, int Hkv, int64_t L, int D, float scale_div,
-                     float* partials, int32_t* counters, void* stream);
+                     void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int D,
+                     float scale_div, float* partials, int32_t* counters, void* stream);
 
 /*
  * RMSNorm of the quantized LLaMA layer (OmniLlamaRMSNorm.forward, quant/omni_norm.py:52-63 of the

@@ -89,7 +89,8 @@ __device__ __forceinline__ float h2f(uint32_t w, int hi) {
 template <int GRP>
 __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
     const float* __restrict__ q, const _Float16* __restrict__ k, const _Float16* __restrict__ v,
-    const _Float16* __restrict__ mask, float* __restrict__ out, int Hq, int Hkv, int L, int chunk,
+    const _Float16* __restrict__ mask, void* __restrict__ out, int out_f16, int Hq, int Hkv,
+    int L, int chunk,
     int S, float scale_div, int* __restrict__ counters, float* __restrict__ part_o,
     float* __restrict__ part_ml) {
   __shared__ float qs[GRP][kD];
@@ -240,10 +241,14 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   __syncthreads();
 
   const int64_t qh0 = (int64_t)b * Hq + (int64_t)hk * GRP;  // first query head of the group
-  float* ob = out + qh0 * kD;
+  // output row of the group: fp32, or rounded once to fp16 (== the reference's .to(fp16))
+  auto put = [&](int o, float val) {
+    if (out_f16) reinterpret_cast<_Float16*>(out)[qh0 * kD + o] = (_Float16)val;
+    else reinterpret_cast<float*>(out)[qh0 * kD + o] = val;
+  };
   if (S == 1) {
     for (int o = tid; o < GRP * kD; o += kThreads)
-      ob[o] = (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD];
+      put(o, (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD]);
     return;
   }
 
@@ -311,7 +316,7 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   }
   __syncthreads();
   for (int o = tid; o < GRP * kD; o += kThreads)
-    ob[o] = (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD];
+    put(o, (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD]);
   if (tid == 0) counters[bh] = 0;  // ready for the next launch (graph replay)
 }
 
@@ -327,10 +332,12 @@ extern "C" int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, i
 }
 
 extern "C" int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v,
-                                const uint16_t* mask, float* out, int64_t B, int Hq, int Hkv,
+                                const uint16_t* mask, void* out, int out_dtype, int64_t B,
+                                int Hq, int Hkv,
                                 int64_t L, int D, float scale_div, float* partials,
                                 int32_t* counters, void* stream) {
-  if (!q || !k || !v || !out || B < 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv || L <= 0 ||
+  if (!q || !k || !v || !out || (out_dtype != QLIN_F32 && out_dtype != QLIN_F16) || B < 0 ||
+      Hq <= 0 || Hkv <= 0 || Hq % Hkv || L <= 0 ||
       L > kMaxL || D != kD || B * Hkv > 0x7fffffff)
     return QLIN_EINVAL;
   const int grp = Hq / Hkv;
@@ -349,7 +356,8 @@ extern "C" int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_
   hipStream_t st = (hipStream_t)stream;
 #define QLIN_A(G)                                                                             \
   hipLaunchKernelGGL((attn_decode_kernel<G>), grid, dim3(kThreads), 0, st, q,                 \
-                     (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out, Hq,    \
+                     (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,        \
+                     out_dtype == QLIN_F16, Hq,                                                 \
                      Hkv, (int)L, sp.chunk, sp.S, scale_div, (int*)counters, part_o, part_ml)
   switch (grp) {
     case 1: QLIN_A(1); break;

@@ -255,7 +255,9 @@ class QuantLlamaAttention(nn.Module):
             # fused decode attention: same fp32 arithmetic as the path below (repeat_kv, QK^T,
             # / sqrt(d), + mask, clamp, softmax, PV) up to summation order
             attn_output = qlin.attn_decode(query_states, key_states, value_states, attention_mask,
-                                           math.sqrt(self.head_dim))
+                                           math.sqrt(self.head_dim),
+                                           out_dtype=act_dtype if act_dtype == torch.float16
+                                           else torch.float32)
             attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
             return self._out(attn_output, residual), None, past_key_value
 

@@ -52,7 +52,8 @@ SIGNATURES = {
     "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
     "qlin_attn_scores_f32": ([_p, _p, _i, _l, _l, _l, _l, _l, ctypes.c_float, _p], _i),
     "qlin_attn_decode_partials_bytes": ([_l, _i, _i, _l], _l),
-    "qlin_attn_decode": ([_p, _p, _p, _p, _p, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p], _i),
+    "qlin_attn_decode": ([_p, _p, _p, _p, _p, _i, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p],
+                         _i),
 }
 
 
@@ -467,9 +468,10 @@ def _attn_counters(device, heads):
     return c
 
 
-def attn_decode(q, k, v, mask, scale_div):
+def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32):
     """softmax(q k^T / scale_div + mask) v for one query token: q fp32 [B, Hq, 1, D], k/v fp16
-    [B, Hkv, L, D], mask fp16 [B, 1, 1, L] or None -> fp32 [B, Hq, 1, D]."""
+    [B, Hkv, L, D], mask fp16 [B, 1, 1, L] or None -> [B, Hq, 1, D] in out_dtype (fp32, or the
+    fp32 result rounded to fp16 in the kernel)."""
     _dev(q, k, v)
     if not attn_decode_supported(q, k, mask):
         raise ValueError("attn_decode: unsupported shapes / dtypes")
@@ -481,7 +483,7 @@ def attn_decode(q, k, v, mask, scale_div):
     if mask is not None:
         m = mask.reshape(B, L).contiguous() if mask.shape[0] == B else \
             mask.expand(B, 1, 1, L).reshape(B, L).contiguous()
-    out = torch.empty(B, Hq, 1, D, dtype=torch.float32, device=q.device)
+    out = torch.empty(B, Hq, 1, D, dtype=out_dtype, device=q.device)
     lib = load_library()
     nbytes = lib.qlin_attn_decode_partials_bytes(B, Hq, Hkv, L)
     if nbytes < 0:
@@ -491,6 +493,7 @@ def attn_decode(q, k, v, mask, scale_div):
         part = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
         cnt = _attn_counters(q.device, B * Hkv)
     rc = lib.qlin_attn_decode(_ptr(q.contiguous()), _ptr(k), _ptr(v), _ptr(m), _ptr(out),
+                              _dtcode(out),
                               B, Hq, Hkv, L, D, float(scale_div), _ptr(part), _ptr(cnt),
                               _stream(q))
     _check(rc, "qlin_attn_decode")

@@ -42,6 +42,9 @@ def test_attn_decode_matches_reference(B, Hq, Hkv, L, masked):
     ref = _ref(q, k, v, mask)
     err = (out.double() - ref).abs().max().item()
     assert err <= 1e-5 * max(1.0, ref.abs().max().item()), err
+    # fp16 output = the fp32 result rounded once (the layer's .to(fp16) before o_proj)
+    out16 = qlin.attn_decode(q, k, v, mask, math.sqrt(128), out_dtype=torch.float16)
+    assert out16.dtype == torch.float16 and torch.equal(out16, out.half())
 
 
 def test_attn_decode_split_counters_reset_under_graph_replay():
