@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--wbits", type=int, default=4)
     ap.add_argument("--group", type=int, default=128)
     ap.add_argument("--fake-quant", action="store_true", help="dense F.linear on W_dq instead of packed")
+    ap.add_argument("--fused", action="store_true",
+                    help="packed + fuse_packed_projections() (fused q/k/v, gate/up+SiLU, epilogues)")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -52,6 +54,9 @@ def main():
     model = build_random_quant_llama(cfg, quant_args(a.wbits, a.group), seed=1, device=dev,
                                      dtype=torch.float16, layer_ids=range(info.lo, info.hi))
     rtn_quantize_(model, pack=not a.fake_quant)
+    if a.fused and not a.fake_quant:
+        for layer in model.layers:
+            layer.fuse_packed_projections()
     g = torch.Generator(device=dev).manual_seed(123)
     wins = [torch.randint(0, a.vocab, (1, a.tokens), device=dev, generator=g)
             for _ in range(a.windows)] if info.first else None
@@ -68,7 +73,8 @@ def main():
         ppl = float(torch.exp(nll.sum() / (a.windows * a.tokens)))
         print(json.dumps({"world": world, "layers": a.layers, "stages": [list(x) for x in
                           [(s.lo, s.hi) for s in [stage_info(a.layers, r, world) for r in range(world)]]],
-                          "mode": "fake-quant" if a.fake_quant else f"packed int{a.wbits} g{a.group}",
+                          "mode": "fake-quant" if a.fake_quant else
+                          f"packed{' fused' if a.fused else ''} int{a.wbits} g{a.group}",
                           "windows": a.windows, "tokens": a.tokens, "ppl": ppl,
                           "ms_per_window": round(dt / a.windows * 1e3, 2),
                           "nll": [round(float(v), 4) for v in nll]}))
