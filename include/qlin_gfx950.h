@@ -55,6 +55,10 @@ extern "C" {
 #define QLIN_WIDE_ZERO          8
 #define QLIN_FLOAT_ZERO        16
 
+/* return codes (hipError_t values; anything else is a HIP error passed through) */
+#define QLIN_OK     0
+#define QLIN_EINVAL 1 /* hipErrorInvalidValue: bad argument, nothing launched */
+
 /* element dtypes */
 #define QLIN_F16 0
 #define QLIN_F32 1

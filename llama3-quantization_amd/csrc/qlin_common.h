@@ -366,7 +366,3 @@ __host__ __device__ inline int zero_mode(int flags) {
   return (flags & QLIN_FLOAT_ZERO) ? qlin::kZFloat
          : (flags & QLIN_WIDE_ZERO) ? qlin::kZWide : qlin::kZNarrow;
 }
-
-// error codes (hipError_t values)
-#define QLIN_OK 0
-#define QLIN_EINVAL 1
