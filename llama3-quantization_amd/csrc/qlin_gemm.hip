@@ -4,9 +4,9 @@
 // y[M, N] = x[M, K] @ W_dq[N, K]^T (+ bias): replaces F.linear at quant/int_linear.py:62 for the
 // prefill / PPL-window shapes (M = 2048 per window, main.py:127-136; M = 65,536 for batch 32).
 //
-// Structure (256-thread block = 4 waves, block tile 128 x 512 (int8: 128 x 256), wave tile 128 x 128
-// (int8: 64 x 128), BK = 128 = one packed k-tile, two LDS stages; wide-in-N waves because B is
-// read packed, 4x cheaper per LDS byte than A):
+// Structure (512-thread block = 8 waves side by side in N, block tile 128 x 256 / 384 / 512
+// (pick_bn; int8: 128 x 256), wave tile 128 x 32 / 48 / 64, BK = 128 = one packed k-tile, two LDS
+// stages; wide-in-N waves because B is read packed, 4x cheaper per LDS byte than A):
 //   - every operand reaches LDS by LDS-DMA (global_load_lds, 16 B per lane): the x tile (BM rows x
 //     256 B, XOR-swizzled per 16-B chunk by (row & 15) through the per-lane SOURCE address, so the
 //     LDS image stays lane-linear per instruction), the packed codes of the 8 row tiles (already
@@ -40,13 +40,13 @@ constexpr int64_t kActFuseMaxN = 16384;  // act fake-quant fused into the GEMV u
 typedef __attribute__((address_space(3))) void* lds_ptr;
 typedef __attribute__((address_space(1))) void* gbl_ptr;
 
-// Wave tiles are 128 rows x 128 (wide) or 64 (narrow) columns: each B fragment dequantized per
-// k-step feeds 8 MFMAs (one per 16-row block), so its 13 VALU fit the issue slots the MFMAs leave
-// free, and the 4 waves sit side by side in N, so every B element is dequantized once per block.
-// WIDE_N: block 128 x 512 (int2/3/4 when the grid has >= 2 blocks per CU); otherwise 128 x 256
-// (twice the blocks; int8 always: twice the code bytes).
-template <int BITS, bool WIDE_N, int NW = 4> struct Cfg {
-  static constexpr int BN = WIDE_N ? 512 : 256;
+// Wave tiles are 128 rows x BN / 8 columns: each B fragment dequantized per k-step feeds 8 MFMAs
+// (one per 16-row block), so its 13 VALU fit the issue slots the MFMAs leave free, and the waves
+// sit side by side in N, so every B element is dequantized once per block.
+// BN_: block 128 x 256, 128 x 384 or 128 x 512 columns (int8: 256 only, twice the code bytes),
+// chosen per launch by pick_bn (whole rounds of blocks over the CUs).
+template <int BITS, int BN_, int NW = 4> struct Cfg {
+  static constexpr int BN = BN_;
   static constexpr int THREADS = 64 * NW;
   static constexpr int WGN = NW, WGM = 1;  // the waves side by side in N: B dequantized once
   static constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -84,7 +84,7 @@ __device__ __forceinline__ int gemm_group_of(const GemmGeo& g, int k) {
 }
 
 // one k-tile's DMA into stage buffer `st`: x tile, packed codes, (scale, zero) words
-template <int BITS, bool WN_, int GPT, int NW>
+template <int BITS, int WN_, int GPT, int NW>
 __device__ __forceinline__ void load_stage(unsigned char* st, const GemmGeo& g, int kt,
                                            const _Float16* __restrict__ x,
                                            const uint32_t* __restrict__ qw,
@@ -144,7 +144,7 @@ __device__ __forceinline__ void read_a(h8 (&a)[MB], const unsigned char* as, int
 }
 
 // FULL: every k-tile lies inside K (K % 128 == 0, chosen per launch): straight-line k-steps
-template <int BITS, bool WN_, int GPT, int ZM, bool FULL, int NW>
+template <int BITS, int WN_, int GPT, int ZM, bool FULL, int NW>
 __device__ __forceinline__ void compute_stage(const unsigned char* st, const GemmGeo& g, int kt,
                                               f4 (&acc)[Cfg<BITS, WN_, NW>::MB][Cfg<BITS, WN_, NW>::NB]) {
   using C = Cfg<BITS, WN_, NW>;
@@ -207,7 +207,7 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 
 // ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
 // the DMA after the first k-tile; the library instantiates ABL = 0 only
-template <int BITS, bool WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4>
+template <int BITS, int WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
@@ -302,7 +302,7 @@ uint32_t group_magic(int group) {
   return (uint32_t)(((1ull << 31) + d - 1) / d);
 }
 
-template <int BITS, bool WN_, int GPT, int ZM>
+template <int BITS, int WN_, int GPT, int ZM>
 int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
   const int tiles_n = (N + Cfg<BITS, WN_>::BN - 1) / Cfg<BITS, WN_>::BN;
@@ -314,25 +314,62 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
                      dim3(64 * kWaves), 0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, \
                      (_Float16*)y, M, N, K, group, group_magic(group), (int)tiles_m, tiles_n, \
                      (const _Float16*)e.res, e.ep)
-  // straight-line k-steps need K % 128 == 0; the wide tile with 2-4 group slots per k-tile then
-  // spills (the per-step checks bound the scheduler), so it keeps the checked form
-  if (K % BK == 0 && !(WN_ && GPT > 1)) QLIN_GL(true);
+  // straight-line k-steps need K % 128 == 0; the wider tiles with 2-4 group slots per k-tile then
+  // spill (the per-step checks bound the scheduler), so they keep the checked form
+  if (K % BK == 0 && !(WN_ > 256 && GPT > 1)) QLIN_GL(true);
   else QLIN_GL(false);
 #undef QLIN_GL
   return (int)hipGetLastError();
 }
 
-constexpr int64_t kWideMinBlocks = 512;  // >= 2 blocks per CU on 256 CUs
+int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
+      n = c;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+// Block width: the stage buffers hold one block per CU, so a launch runs in rounds of `CUs`
+// blocks.  Cost model fitted on int4 g128 (tools/dev/gemm_bn.py, MI355X): a full round of
+// 128 x 256 / 384 / 512 blocks takes 1 / 1.42 / 1.84 units (wider blocks dequantize each B
+// fragment for more MFMAs), and a partial round with a fraction f of the CUs busy takes
+// (0.5 + 0.5 f) of a full one (less contention for L2 / HBM).  M = 2048: N = 4096 -> 256 (one
+// round), N = 6144 -> 384 (one round instead of 1.5: 121 -> 97 us), N = 14336 / 28672 -> 512;
+// M >= 8192 -> 512.
+int pick_bn(int64_t M, int N, int bits) {
+  if (bits == 8) return 256;
+  const int64_t tm = (M + BM - 1) / BM, cus = cu_count();
+  static const int bn[3] = {256, 384, 512};
+  static const double rel[3] = {1.0, 1.42, 1.84};
+  int best = 256;
+  double best_cost = 0;
+  for (int i = 0; i < 3; ++i) {
+    const int64_t blocks = tm * ((N + bn[i] - 1) / bn[i]);
+    const int64_t full = blocks / cus;
+    const double f = (double)(blocks - full * cus) / (double)cus;
+    const double cost = rel[i] * ((double)full + (f > 0 ? 0.5 + 0.5 * f : 0.0));
+    if (i == 0 || cost < best_cost) best = bn[i], best_cost = cost;
+  }
+  return best;
+}
 
 template <int BITS, int GPT, int ZM>
 int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                 uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
   if constexpr (BITS != 8) {
-    const int64_t wide_blocks = ((M + BM - 1) / BM) * ((N + 511) / 512);
-    if (wide_blocks >= kWideMinBlocks)
-      return launch_gemm_t<BITS, true, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+    const int bn = pick_bn(M, N, BITS);
+    if (bn == 512)
+      return launch_gemm_t<BITS, 512, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+    if (bn == 384)
+      return launch_gemm_t<BITS, 384, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   }
-  return launch_gemm_t<BITS, false, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+  return launch_gemm_t<BITS, 256, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
 }
 
 template <int BITS, int ZM>

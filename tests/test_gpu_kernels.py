@@ -220,16 +220,31 @@ def test_gptq_checkpoint_conversion(bits, group):
     assert_close_to_ref(n(y), O.linear_ref(x, ref_w, tensors["lin.bias"].numpy()))
 
 
+def _pick_bn(M, N, cus=256):
+    """Mirror of qlin_gemm.hip pick_bn (block width by rounds of blocks over the CUs)."""
+    rel = {256: 1.0, 384: 1.42, 512: 1.84}
+    best = None
+    for bn in (256, 384, 512):
+        blocks = -(-M // 128) * -(-N // bn)
+        full, f = blocks // cus, (blocks % cus) / cus
+        c = rel[bn] * (full + (0.5 + 0.5 * f if f else 0.0))
+        if best is None or c < best[1]:
+            best = (bn, c)
+    return best[0]
+
+
+@pytest.mark.parametrize("M,N,bn", [(4129, 6160, 512), (4129, 4112, 384), (8225, 4240, 256)])
 @pytest.mark.parametrize("bits,group", [(4, 128), (4, 64), (3, 64), (2, 32)])
-def test_gemm_wide_tile(bits, group):
-    """The 128 x 512 block tile (taken when the grid has >= 2 blocks per CU: the configs[2]
-    shape) with ragged M and N; g64 / g32 take its checked k-step form."""
-    M, N, K = 8192 + 33, 4096 + 16, 1024
+def test_gemm_block_widths(bits, group, M, N, bn):
+    """The 128 x 256 / 384 / 512 block tiles (pick_bn: whole rounds of blocks over 256 CUs) with
+    ragged M and N; g64 / g32 take the wider tiles' checked k-step form."""
+    assert _pick_bn(M, N) == bn
+    K = 1024
     qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=bits + group)
     x = rand_x(M, K, seed=7)
     y = n(qlin.gemm(t(x), qw, qsz, None, N, K, bits, group, fl))
     rows = np.r_[0:64, M // 2 - 64:M // 2 + 64, M - 96:M]  # a sample of rows keeps the fp64 ref cheap
-    assert_close_to_ref(y[rows], O.linear_ref(x[rows], wdq), what=f"wide gemm b{bits} g{group}")
+    assert_close_to_ref(y[rows], O.linear_ref(x[rows], wdq), what=f"gemm bn{bn} b{bits} g{group}")
 
 
 @pytest.mark.parametrize("N", [8192 + 16 * 3 + 5, 8192 + 16])

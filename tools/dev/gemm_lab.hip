@@ -6,6 +6,13 @@ extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
   // abl bit 2: the wide (128 x 512) tile; bit 3: 8 waves per block (else 4)
   const bool wn = abl & 4;
   const bool w8 = abl & 8;
+  if (abl & 16) {  // bit 4: the 128 x 384 tile, 8 waves, no ablation
+    const int tn = (N + 383) / 384, tm = (int)((M + BM - 1) / BM);
+    hipLaunchKernelGGL((gemm_kernel<4, 384, 1, kZNarrow, true, 0, 8>), dim3(tm * tn), dim3(512), 0,
+                       (hipStream_t)stream, qw, qsz, (const _Float16*)x, nullptr, (_Float16*)y, M,
+                       N, K, 128, group_magic(128), tm, tn, nullptr, 0);
+    return (int)hipGetLastError();
+  }
   const int tiles_n = (N + (wn ? 512 : 256) - 1) / (wn ? 512 : 256);
   const int tiles_m = (int)((M + BM - 1) / BM);
   const dim3 grid(tiles_m * tiles_n);
@@ -16,8 +23,8 @@ extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
 #define LA(W, NW) \
   { if (a == 0) L(W, 0, NW); else if (a == 1) L(W, 1, NW); else if (a == 2) L(W, 2, NW); else L(W, 3, NW); }
   const int a = abl & 3;
-  if (w8) { if (wn) LA(true, 8) else LA(false, 8) }
-  else { if (wn) LA(true, 4) else LA(false, 4) }
+  if (w8) { if (wn) LA(512, 8) else LA(256, 8) }
+  else { if (wn) LA(512, 4) else LA(256, 4) }
 #undef LA
 #undef L
   return (int)hipGetLastError();
