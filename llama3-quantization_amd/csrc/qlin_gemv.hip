@@ -405,12 +405,13 @@ uint32_t group_magic(int group) {
   return (uint32_t)(((1ull << 31) + d - 1) / d);
 }
 
-// waves per block: grow W until the grid holds ~32 waves for each of the 256 CUs (measured on
-// the decode layer's shapes, tools/dev/gemv_geo.py: N = 28,672 x K = 4,096 W = 8 12.6 us vs
-// W = 4 13.3 us; 4096 x 4096 and 6144 x 4096 keep W = 16)
+// waves per block: grow W until the grid holds ~32 waves for each of the 256 CUs; on grids of
+// >= 512 row tiles keep >= 4 tiles per wave (measured on the decode layer's shapes,
+// tools/dev/gemv_geo.py: 28,672 x 4,096 W = 8 12.6 us vs W = 4 13.3 us; 14,336 x 4,096 W = 8
+// 8.9 us vs W = 16 9.3 us; 4096 x 4096 and 6144 x 4096 keep W = 16)
 int pick_waves(int Nt, int Kt, int& tpw) {
   int W = 1;
-  while (W < kMaxWaves && (int64_t)Nt * W < 8192) W *= 2;
+  while (W < kMaxWaves && (int64_t)Nt * W < 8192 && (Nt < 512 || Kt >= 8 * W)) W *= 2;
   W = min(W, Kt);
   tpw = (Kt + W - 1) / W;
   return (Kt + tpw - 1) / tpw;
@@ -437,8 +438,11 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
     if (ntb == 2) QLIN_GV(2, 2);
     else QLIN_GV(2, 1);
   } else {
-    if (tpw <= 2) QLIN_GV(2, 1);
-    else QLIN_GV(4, 1);
+    // four tiles in flight where the wave's tiles come in whole rounds of four (or many of
+    // them): 4096 x 14,336 (tpw 7) PF = 2 7.95 us vs PF = 4 8.46 us; 28,672 x 4,096 (tpw 4)
+    // and tpw 14 prefer four
+    if (tpw % 4 == 0 || tpw >= 12) QLIN_GV(4, 1);
+    else QLIN_GV(2, 1);
   }
 #undef QLIN_GV
   return (int)hipGetLastError();

@@ -65,5 +65,7 @@ for (N, K) in SHAPES:
                     us = timed(lambda: [lib.geo_gemv(P(m[0].data_ptr()), P(m[1].data_ptr()), P(x.data_ptr()),
                                                      P(y.data_ptr()), M, N, K, W, PF, NTB, st()) for m in mats], R)
                     print(f"   NTB={NTB} W={W:2d} PF={PF}: {us:.2f} us ({nbytes / us / 1e3:.0f} GB/s)", flush=True)
+        prod = timed(lambda: [qlin.gemv(x, m[0], m[1], None, N, K, 4, 128) for m in mats], R)
+        print(f"   product again: {prod:.2f} us ({nbytes / prod / 1e3:.0f} GB/s)", flush=True)
     del mats
     torch.cuda.empty_cache()
