@@ -33,7 +33,7 @@ namespace {
 // N = K = 4096): M = 2048 narrow 923 -> 1010, M = 16384 wide 1021 -> 1135, M = 65536 wide
 // 1049 -> 1112 TFLOP/s.
 constexpr int kWaves = 8;
-constexpr int BM = 128, BK = kTileK;  // block rows; one packed k-tile per stage
+constexpr int BK = kTileK;  // one packed k-tile per stage
 constexpr int64_t kSkinnyMaxM = 64;   // qlin_linear_f16: M <= this runs the GEMV kernel
 constexpr int64_t kActFuseMaxN = 16384;  // act fake-quant fused into the GEMV up to this N
 
@@ -45,8 +45,11 @@ typedef __attribute__((address_space(1))) void* gbl_ptr;
 // sit side by side in N, so every B element is dequantized once per block.
 // BN_: block 128 x 256, 128 x 384 or 128 x 512 columns (int8: 256 only, twice the code bytes),
 // chosen per launch by pick_bn (whole rounds of blocks over the CUs).
+// BN_ = 128: the 64 x 128 block for grids that leave most CUs idle at 128 x 256 (fewer rows
+// and columns per block, the same k order per output).
 template <int BITS, int BN_, int NW = 4> struct Cfg {
   static constexpr int BN = BN_;
+  static constexpr int BM = BN_ == 128 ? 64 : 128;  // block rows
   static constexpr int THREADS = 64 * NW;
   static constexpr int WGN = NW, WGM = 1;  // the waves side by side in N: B dequantized once
   static constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -96,12 +99,12 @@ __device__ __forceinline__ void load_stage(unsigned char* st, const GemmGeo& g, 
   {
     const int sub = g.lane >> 4, p = g.lane & 15;
 #pragma unroll
-    for (int j = 0; j < BM / (4 * NW); ++j) {
-      const int r = (BM / NW) * g.wave + 4 * j + sub;  // LDS row
+    for (int j = 0; j < C::BM / (4 * NW); ++j) {
+      const int r = (C::BM / NW) * g.wave + 4 * j + sub;  // LDS row
       const int c = p ^ (r & 15);                      // logical chunk held at physical p
       const int64_t m = min(g.m0 + r, g.M - 1);
       const int k = min(kt * BK + 8 * c, g.K - 8);
-      glds16(x + m * g.K + k, st + ((BM / NW) * g.wave + 4 * j) * 256);
+      glds16(x + m * g.K + k, st + ((C::BM / NW) * g.wave + 4 * j) * 256);
     }
   }
   // packed codes: RT row tiles x 256*BITS bytes, lane-linear 16-B chunks
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
   int lb = b;
   if ((nblk & 7) == 0) lb = (b & 7) * (nblk >> 3) + (b >> 3);
   const int tile_m = lb / tiles_n, tile_n = lb - tile_m * tiles_n;
-  g.m0 = (int64_t)tile_m * BM;
+  g.m0 = (int64_t)tile_m * C::BM;
   g.nt0 = (int64_t)tile_n * C::RT;
   g.ntl = (N + kTileN - 1) / kTileN - 1;
 
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
     }
     return;
   }
-  if (g.m0 + BM <= M && (int64_t)BM * N < (1ll << 31)) {
+  if (g.m0 + C::BM <= M && (int64_t)C::BM * N < (1ll << 31)) {
     // whole row tile inside M: a uniform row base and 32-bit per-lane offsets, no row checks
     // (M = 65,536: 1151 -> 1206 TFLOP/s against the per-element checked stores below)
     const int64_t base = (g.m0 + wm * C::WM) * (int64_t)N;
@@ -339,7 +342,7 @@ template <int BITS, int WN_, int GPT, int ZM>
 int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
   const int tiles_n = (N + Cfg<BITS, WN_>::BN - 1) / Cfg<BITS, WN_>::BN;
-  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t tiles_m = (M + Cfg<BITS, WN_>::BM - 1) / Cfg<BITS, WN_>::BM;
   const int64_t blocks = tiles_m * tiles_n;
   if (blocks > 0x7fffffff) return QLIN_EINVAL;
 #define QLIN_GL(KF)                                                                           \
@@ -375,9 +378,13 @@ int cu_count() {
 // (0.5 + 0.5 f) of a full one (less contention for L2 / HBM).  M = 2048: N = 4096 -> 256 (one
 // round), N = 6144 -> 384 (one round instead of 1.5: 121 -> 97 us), N = 14336 / 28672 -> 512;
 // M >= 8192 -> 512.
+// Grids of 128 x 256 blocks that leave half the CUs or more idle take 64 x 128 blocks, four
+// times as many (tools/dev/gemm_bn.py, int4 g128 K = 4096): the GQA k / v projection N = 1024 at
+// M = 2048 53 -> 29 us; N = 4096 at M = 128-512 50 -> 24-32 us, M = 1024 57 -> 52 us.
 int pick_bn(int64_t M, int N, int bits) {
   if (bits == 8) return 256;
-  const int64_t tm = (M + BM - 1) / BM, cus = cu_count();
+  const int64_t tm = (M + 127) / 128, cus = cu_count();
+  if (tm * ((N + 255) / 256) * 2 <= cus) return 128;
   static const int bn[3] = {256, 384, 512};
   static const double rel[3] = {1.0, 1.42, 1.84};
   int best = 256;
@@ -401,6 +408,8 @@ int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
       return launch_gemm_t<BITS, 512, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
     if (bn == 384)
       return launch_gemm_t<BITS, 384, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+    if (bn == 128)
+      return launch_gemm_t<BITS, 128, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   }
   return launch_gemm_t<BITS, 256, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
 }

@@ -221,7 +221,10 @@ def test_gptq_checkpoint_conversion(bits, group):
 
 
 def _pick_bn(M, N, cus=256):
-    """Mirror of qlin_gemm.hip pick_bn (block width by rounds of blocks over the CUs)."""
+    """Mirror of qlin_gemm.hip pick_bn (block width by rounds of blocks over the CUs; 128 = the
+    64 x 128 block for small grids)."""
+    if -(-M // 128) * -(-N // 256) * 2 <= cus:
+        return 128
     rel = {256: 1.0, 384: 1.42, 512: 1.84}
     best = None
     for bn in (256, 384, 512):
@@ -233,17 +236,18 @@ def _pick_bn(M, N, cus=256):
     return best[0]
 
 
-@pytest.mark.parametrize("M,N,bn", [(4129, 6160, 512), (4129, 4112, 384), (8225, 4240, 256)])
+@pytest.mark.parametrize("M,N,bn", [(4129, 6160, 512), (4129, 4112, 384), (8225, 4240, 256),
+                                    (333, 1040, 128), (65, 4112, 128)])
 @pytest.mark.parametrize("bits,group", [(4, 128), (4, 64), (3, 64), (2, 32)])
 def test_gemm_block_widths(bits, group, M, N, bn):
-    """The 128 x 256 / 384 / 512 block tiles (pick_bn: whole rounds of blocks over 256 CUs) with
-    ragged M and N; g64 / g32 take the wider tiles' checked k-step form."""
+    """The 128 x 256 / 384 / 512 and 64 x 128 block tiles (pick_bn: whole rounds of blocks over
+    256 CUs) with ragged M and N; g64 / g32 take the wider tiles' checked k-step form."""
     assert _pick_bn(M, N) == bn
     K = 1024
     qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=bits + group)
     x = rand_x(M, K, seed=7)
     y = n(qlin.gemm(t(x), qw, qsz, None, N, K, bits, group, fl))
-    rows = np.r_[0:64, M // 2 - 64:M // 2 + 64, M - 96:M]  # a sample of rows keeps the fp64 ref cheap
+    rows = np.unique(np.r_[0:64, M // 2 - 64:M // 2 + 64, M - 96:M].clip(0, M - 1))  # fp64 ref sample
     assert_close_to_ref(y[rows], O.linear_ref(x[rows], wdq), what=f"gemm bn{bn} b{bits} g{group}")
 
 

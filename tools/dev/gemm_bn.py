@@ -40,7 +40,7 @@ for (N, K) in SHAPES:
 
     x = torch.randn(333, K, device=dev, dtype=torch.float16)
     ref = qlin.gemm(x, o["qweight"], o["qsz"], None, N, K, 4, 128)
-    for v in (8, 12, 16):
+    for v in (8, 12, 16, 32):
         y = torch.zeros_like(ref)
         assert run(v, 333, x, y) == 0
         torch.cuda.synchronize()
@@ -52,7 +52,7 @@ for (N, K) in SHAPES:
         f = 2 * M * N * K
         reps = max(3, min(50, int(4e12 / f)))
         t = {name: timeit(lambda: run(v, M, x, y), reps) for name, v in
-             (("256", 8), ("384", 16), ("512", 12))}
+             (("64x128", 32), ("256", 8), ("384", 16), ("512", 12))}
         t["product"] = timeit(lambda: qlin.gemm(x, o["qweight"], o["qsz"], None, N, K, 4, 128), reps)
         print(f"N={N} K={K} M={M}: " + "  ".join(f"{k} {v*1e6:.1f} us ({f/v/1e12:.0f})" for k, v in t.items()),
               flush=True)

@@ -6,15 +6,22 @@ extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
   // abl bit 2: the wide (128 x 512) tile; bit 3: 8 waves per block (else 4)
   const bool wn = abl & 4;
   const bool w8 = abl & 8;
+  if (abl & 32) {  // bit 5: the 64 x 128 tile, 8 waves, no ablation
+    const int tn = (N + 127) / 128, tm = (int)((M + 63) / 64);
+    hipLaunchKernelGGL((gemm_kernel<4, 128, 1, kZNarrow, true, 0, 8>), dim3(tm * tn), dim3(512), 0,
+                       (hipStream_t)stream, qw, qsz, (const _Float16*)x, nullptr, (_Float16*)y, M,
+                       N, K, 128, group_magic(128), tm, tn, nullptr, 0);
+    return (int)hipGetLastError();
+  }
   if (abl & 16) {  // bit 4: the 128 x 384 tile, 8 waves, no ablation
-    const int tn = (N + 383) / 384, tm = (int)((M + BM - 1) / BM);
+    const int tn = (N + 383) / 384, tm = (int)((M + 127) / 128);
     hipLaunchKernelGGL((gemm_kernel<4, 384, 1, kZNarrow, true, 0, 8>), dim3(tm * tn), dim3(512), 0,
                        (hipStream_t)stream, qw, qsz, (const _Float16*)x, nullptr, (_Float16*)y, M,
                        N, K, 128, group_magic(128), tm, tn, nullptr, 0);
     return (int)hipGetLastError();
   }
   const int tiles_n = (N + (wn ? 512 : 256) - 1) / (wn ? 512 : 256);
-  const int tiles_m = (int)((M + BM - 1) / BM);
+  const int tiles_m = (int)((M + 127) / 128);
   const dim3 grid(tiles_m * tiles_n);
 #define L(W, A, NW)                                                                             \
   hipLaunchKernelGGL((gemm_kernel<4, W, 1, kZNarrow, true, A, NW>), grid, dim3(64 * NW), 0,     \
