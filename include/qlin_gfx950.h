@@ -146,6 +146,13 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
                     int group, void* stream);
 
 /*
+ * Output columns per block that qlin_gemm_f16 picks for an M x N launch on the current device
+ * (128, 256, 384 or 512; 128 = the 64-row x 128-column block for small grids), or -1 for invalid
+ * arguments.  Introspection for tests and tools; no reference counterpart.
+ */
+int qlin_gemm_block_cols(int64_t M, int64_t N, int bits);
+
+/*
  * The packed linear with a fused output epilogue (the decoder layer's glue around two of its
  * linears, models/int_llama_layer.py of the reference) and optional activation fake-quant:
  *   QLIN_EP_RESIDUAL  y = RN16(residual + RN16(x @ W_dq^T + bias)) — o_proj / down_proj followed

@@ -4,9 +4,10 @@
 // y[M, N] = x[M, K] @ W_dq[N, K]^T (+ bias): replaces F.linear at quant/int_linear.py:62 for the
 // prefill / PPL-window shapes (M = 2048 per window, main.py:127-136; M = 65,536 for batch 32).
 //
-// Structure (512-thread block = 8 waves side by side in N, block tile 128 x 256 / 384 / 512
-// (pick_bn; int8: 128 x 256), wave tile 128 x 32 / 48 / 64, BK = 128 = one packed k-tile, two LDS
-// stages; wide-in-N waves because B is read packed, 4x cheaper per LDS byte than A):
+// Structure (512-thread block = 8 waves side by side in N, block tile 128 x 256 / 384 / 512, or
+// 64 x 128 for grids that would leave most CUs idle (pick_bn; int8: 128 x 256), wave tile
+// 128 x 32 / 48 / 64 (64 x 16), BK = 128 = one packed k-tile, two LDS stages; wide-in-N waves
+// because B is read packed, 4x cheaper per LDS byte than A):
 //   - every operand reaches LDS by LDS-DMA (global_load_lds, 16 B per lane): the x tile (BM rows x
 //     256 B, XOR-swizzled per 16-B chunk by (row & 15) through the per-lane SOURCE address, so the
 //     LDS image stays lane-linear per instruction), the packed codes of the 8 row tiles (already
@@ -22,6 +23,7 @@
 #include "qlin_common.h"
 #include "../../include/qlin_gfx950.h"
 
+#include <atomic>
 #include <type_traits>
 
 using namespace qlin;
@@ -358,28 +360,32 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   return (int)hipGetLastError();
 }
 
+// CUs of the current device, cached per device id (the first call per device queries it; racing
+// first calls store the same value)
 int cu_count() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0, c = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
-      n = c;
-    else
-      n = 256;
-  }
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  int n = dev < kMaxDev ? cache[dev].load(std::memory_order_relaxed) : 0;
+  if (n > 0) return n;
+  int c = 0;
+  n = (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+       c > 0) ? c : 256;
+  if (dev < kMaxDev) cache[dev].store(n, std::memory_order_relaxed);
   return n;
 }
 
-// Block width: the stage buffers hold one block per CU, so a launch runs in rounds of `CUs`
-// blocks.  Cost model fitted on int4 g128 (tools/dev/gemm_bn.py, MI355X): a full round of
-// 128 x 256 / 384 / 512 blocks takes 1 / 1.42 / 1.84 units (wider blocks dequantize each B
-// fragment for more MFMAs), and a partial round with a fraction f of the CUs busy takes
-// (0.5 + 0.5 f) of a full one (less contention for L2 / HBM).  M = 2048: N = 4096 -> 256 (one
-// round), N = 6144 -> 384 (one round instead of 1.5: 121 -> 97 us), N = 14336 / 28672 -> 512;
-// M >= 8192 -> 512.
+// Block width.  The 128 x 256 / 384 / 512 blocks use 2 x 48-72 KB of LDS stages, so one block
+// fits a CU and a launch runs in rounds of `CUs` blocks.  Cost model fitted on int4 g128
+// (tools/dev/gemm_bn.py, MI355X): a full round of 128 x 256 / 384 / 512 blocks takes 1 / 1.42 /
+// 1.84 units (wider blocks dequantize each B fragment for more MFMAs), and a partial round with a
+// fraction f of the CUs busy takes (0.5 + 0.5 f) of a full one (less contention for L2 / HBM).
+// M = 2048: N = 4096 -> 256 (one round), N = 6144 -> 384 (one round instead of 1.5: 121 -> 97
+// us), N = 14336 / 28672 -> 512; M >= 8192 -> 512.
 // Grids of 128 x 256 blocks that leave half the CUs or more idle take 64 x 128 blocks, four
-// times as many (tools/dev/gemm_bn.py, int4 g128 K = 4096): the GQA k / v projection N = 1024 at
+// times as many (2 x 13-16 KB stages: three blocks fit a CU, so the round model above does not
+// apply to them; tools/dev/gemm_bn.py, int4 g128 K = 4096): the GQA k / v projection N = 1024 at
 // M = 2048 53 -> 29 us; N = 4096 at M = 128-512 50 -> 24-32 us, M = 1024 57 -> 52 us.
 int pick_bn(int64_t M, int N, int bits) {
   if (bits == 8) return 256;
@@ -454,6 +460,12 @@ int gemm_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint1
 }
 }  // namespace
 
+extern "C" int qlin_gemm_block_cols(int64_t M, int64_t N, int bits) {
+  if (M < 1 || N < 1 || N > (1 << 30) || !(bits == 2 || bits == 3 || bits == 4 || bits == 8))
+    return -QLIN_EINVAL;
+  return pick_bn(M, (int)N, bits);
+}
+
 extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                              const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
                              int64_t N, int64_t K, int bits, int group, void* workspace,
@@ -467,8 +479,8 @@ extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int
                                int64_t N, int64_t K, int bits, int group, void* stream) {
   if (M == 0) return QLIN_OK;
   if (M <= kSkinnyMaxM) {
-    // skinny batches: the GEMV kernel in 16-row chunks (weights re-streamed per chunk, still far
-    // better parallelised than the GEMM's 256-row tiles for these M)
+    // skinny batches: the GEMV kernel in 16-row chunks (weights re-streamed per chunk; a 64-row
+    // GEMM block alone on its CU is issue-bound at ~24 us for K = 4096)
     for (int64_t m0 = 0; m0 < M; m0 += 16) {
       const int64_t mc = M - m0 < 16 ? M - m0 : 16;
       const int rc = qlin_gemv_f16(qweight, qsz, flags, x + m0 * K, bias, y + m0 * N, mc, N, K,

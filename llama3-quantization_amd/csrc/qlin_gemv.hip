@@ -361,6 +361,152 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Decode fast path: M <= 4, K % 128 == 0, group % 128 == 0 or group in {32, 64}, no activation
+// fake-quant.  Same arithmetic as gemv_kernel (exact W_dq, one MFMA per k-step), built for the
+// ~3-4 us a 4096 x 4096 launch lasts (tools/dev/gemv_lab2.hip, gemv_lab3.hip):
+//   - everything the general kernel derives by integer division (tiles, groups, strides) comes
+//     precomputed from the host, so the first weight load issues a few scalar ops after the
+//     kernel arguments land; the epilogue is a template parameter, so the executed code is one
+//     short straight line (the weights arrive ~1 us after the start: code fetched late, or work
+//     queued in front of the loads, shows up 1:1 in the launch time);
+//   - wave w streams tiles kt = w, w + W, w + 2W, ...: the tiles in flight on a CU at one time
+//     are W tiles (W x 1 KB for int4) apart in HBM instead of adjacent (4096^2: 3.89 -> 3.74 us);
+//   - all codes of the prefetch window are issued before their (scale, zero) words and x, so the
+//     first tile only waits for its own three loads.
+// ---------------------------------------------------------------------------------------------
+struct FastArgs {
+  const uint32_t* qw;   // row tile 0 of qweight
+  const uint32_t* qsz;  // row tile 0 of qsz
+  const _Float16* x;
+  const _Float16* bias;
+  const _Float16* res;
+  _Float16* y;
+  int M, N, K, Kt, G;
+  int W, lw;            // waves per block (power of two), log2 W
+  uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
+};
+
+// every wave streams at most PF tiles, all of them loaded up front (no refill loop: a launch whose
+// waves need more tiles takes gemv_kernel, whose contiguous tile runs stream better then)
+template <int BITS, int MT, int GPT, int ZM, int EP, int PF>
+__global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
+  __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, n_in = lane & 15;
+  const int nt = blockIdx.x;
+  const uint32_t* qw = a.qw + (int64_t)nt * a.Kt * (64 * BITS) + lane * BITS;
+  const uint32_t* sz = a.qsz + (int64_t)nt * a.G * kTileN + n_in;
+  constexpr int LPR = 64 / MT;  // lanes per x row
+  const _Float16* xr = a.x + (int64_t)min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
+  const int nts = (a.Kt - wave + a.W - 1) >> a.lw;  // >= 1: W <= Kt
+  const int ktl = wave + ((nts - 1) << a.lw);        // the wave's last tile
+
+  auto kt_of = [&](int i) { return min(wave + (i << a.lw), ktl); };
+  auto group_of_tile = [&](int kt) {
+    return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
+  };
+  WTile<BITS, GPT> wt[PF];
+  XRaw<MT> xq[PF];
+  auto load_codes = [&](int u, int kt) { wt[u].pc = load_piece_nt<BITS>(qw + kt * (64 * BITS)); };
+  auto load_rest = [&](int u, int kt) {
+    const int g0 = group_of_tile(kt);
+#pragma unroll
+    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = sz[(g0 + s) * kTileN];
+    const _Float16* p = xr + kt * kTileK;
+    if constexpr (MT == 1) {
+      xq[u].w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (MT == 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      xq[u].w[0] = v.x; xq[u].w[1] = v.y;
+    } else {
+      const uint4 v = *reinterpret_cast<const uint4*>(p);
+      xq[u].w[0] = v.x; xq[u].w[1] = v.y; xq[u].w[2] = v.z; xq[u].w[3] = v.w;
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_rest(u, kt_of(u));
+  // the epilogue's bias / residual operands, fetched while the weights stream (fetched after the
+  // reduction they would cost one more round trip).  Only wave 0's lanes use them, but every wave
+  // loads (clamped, L2-resident): a load under a branch is waited for at the branch's join
+  constexpr int NO = EP == kEpSiluMul ? MT * 8 : MT * kTileN;  // outputs per block
+  const int om = min(tid / (NO / MT), a.M - 1), on = tid % (NO / MT);  // output (row m, column n)
+  const int64_t orow = (int64_t)nt * kTileN + on;
+  const bool oval = tid < NO && tid / (NO / MT) < a.M && orow + (EP == kEpSiluMul ? 8 : 0) < a.N;
+  const _Float16* bsrc = a.bias ? a.bias + min(orow, (int64_t)a.N - 1) : a.x;
+  const _Float16 ob0 = bsrc[0];
+  const _Float16 ob1 = EP == kEpSiluMul ? bsrc[a.bias ? 8 : 0] : ob0;
+  _Float16 ores = 0;
+  if constexpr (EP == kEpResidual) ores = a.res[(int64_t)om * a.N + min(orow, (int64_t)a.N - 1)];
+
+  const Magics mg = make_magics<BITS>();
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  uint32_t* slot = &xs[wave][0];
+  auto tile = [&](int u) {
+    h8 xa[4];
+    park_x<MT>(xa, xq[u], slot, lane, n_in);
+    auto step = [&](auto S_) {
+      constexpr int S = decltype(S_)::value;
+      uint32_t v[4];
+      const GroupQ gq = make_group_w<BITS, ZM>(wt[u].sz[S * GPT / 4]);
+      dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
+      const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, acc, 0, 0, 0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+  };
+  // every slot is computed — a slot past the wave's tiles (a repeat of its last tile) with x
+  // zeroed — so the compiler cannot sink those slots' loads behind a branch (which it does for
+  // `if (u < nts) tile(u)`: the loads then issue only after the earlier tiles' compute, one
+  // extra HBM round trip per launch)
+  tile(0);  // nts >= 1
+#pragma unroll
+  for (int u = 1; u < PF; ++u) {
+    if (u >= nts) {  // wave-uniform
+#pragma unroll
+      for (int c = 0; c < MT; ++c) xq[u].w[c] = 0u;
+    }
+    tile(u);
+  }
+
+  // combine the W partials of (row m, column n): C row m = 4q + e sits in lane n + 16q, element e
+  const int q4 = 4 * (lane >> 4);
+  if (q4 < MT) {
+#pragma unroll
+    for (int e = 0; e < 4 && e < MT; ++e) red[((q4 + e) * kTileN + n_in) * kMaxWaves + wave] = acc[e];
+    if (wave == 0)
+      for (int w = a.W; w < kMaxWaves; ++w)
+#pragma unroll
+        for (int e = 0; e < 4 && e < MT; ++e) red[((q4 + e) * kTileN + n_in) * kMaxWaves + w] = 0.f;
+  }
+  __syncthreads();
+  auto total = [&](int o, _Float16 b) {
+    const f4* r = reinterpret_cast<const f4*>(red + o * kMaxWaves);
+    const f4 p = r[0], q = r[1], c = r[2], d = r[3];
+    const f4 e = (p + q) + (c + d);
+    float t = (e[0] + e[1]) + (e[2] + e[3]);
+    if (a.bias) t += (float)b;
+    return (float)(_Float16)t;  // F.linear's fp16 output
+  };
+  if (oval) {  // wave 0 only (tid < NO <= 64)
+    if constexpr (EP == kEpSiluMul) {  // 8 outputs per tile and row
+      const float g = total(om * kTileN + on, ob0), u = total(om * kTileN + on + 8, ob1);
+      a.y[(int64_t)om * (a.N >> 1) + nt * 8 + on] = (_Float16)(silu_rn16(g) * u);
+    } else {
+      float t = total(om * kTileN + on, ob0);
+      if constexpr (EP == kEpResidual) t += (float)ores;
+      a.y[(int64_t)om * a.N + orow] = (_Float16)t;
+    }
+  }
+}
+
 // standalone exact dequant: one thread per lane piece -> 4 x 8 fp16 values of one row
 template <int BITS, int ZM>
 __global__ __launch_bounds__(256) void dequant_kernel(
@@ -448,6 +594,67 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   return (int)hipGetLastError();
 }
 
+// the decode fast path (gemv_fast_kernel): M <= 4, K % 128 == 0, whole or 32 / 64-wide groups
+bool fast_ok(int M, int K, int group, const Ep& e) {
+  return M <= 4 && K % kTileK == 0 && !e.aq.on &&
+         (group % kTileK == 0 || group == 32 || group == 64);
+}
+
+template <int BITS, int MT, int GPT, int ZM, int EP>
+int launch_fast_t(const FastArgs& a, int Nt, int tpw, hipStream_t st) {
+#define QLIN_GF(PF)                                                                           \
+  hipLaunchKernelGGL((gemv_fast_kernel<BITS, MT, GPT, ZM, EP, PF>), dim3(Nt), dim3(64 * a.W), \
+                     0, st, a)
+  if (tpw <= 2) QLIN_GF(2);
+  else QLIN_GF(4);
+#undef QLIN_GF
+  return (int)hipGetLastError();
+}
+
+// fast-path geometry: pick_waves rounded down to a power of two; the fast path takes launches
+// whose waves stream at most 4 tiles (tools/dev/fast_geo.py, M = 1: 4096 x 4096 W = 16 x 2 tiles
+// 4.30 -> 3.76 us, 6144 x 4096 5.48 -> 5.02, 28672 x 4096 W = 8 x 4 13.55 -> 12.67; the
+// LLaMA down projection 4096 x 14336, 7 tiles per wave, stays on gemv_kernel: 7.8 vs 8.3 us)
+bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
+  W = pick_waves(Nt, Kt, tpw);
+  lw = 0;
+  while ((2 << lw) <= W) ++lw;  // round W down to a power of two (W <= Kt)
+  W = 1 << lw;
+  tpw = (Kt + W - 1) / W;
+  return tpw <= 4;
+}
+
+template <int BITS, int MT, int ZM>
+int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
+                uint16_t* y, int M, int N, int K, int group, int W, int lw, int tpw,
+                hipStream_t st, const Ep& e) {
+  const int Nt = (N + kTileN - 1) / kTileN;
+  FastArgs a;
+  a.qw = qw;
+  a.qsz = qsz;
+  a.x = (const _Float16*)x;
+  a.bias = (const _Float16*)bias;
+  a.res = (const _Float16*)e.res;
+  a.y = (_Float16*)y;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.Kt = K / kTileK;
+  a.G = K / group;
+  a.W = W;
+  a.lw = lw;
+  const uint64_t c = group % kTileK == 0 ? (uint64_t)(group / kTileK) : 1;
+  a.cmagic = (uint32_t)(((1ull << 31) + c - 1) / c);
+#define QLIN_FE(GPT)                                                                           \
+  return e.ep == kEpResidual  ? launch_fast_t<BITS, MT, GPT, ZM, kEpResidual>(a, Nt, tpw, st)  \
+         : e.ep == kEpSiluMul ? launch_fast_t<BITS, MT, GPT, ZM, kEpSiluMul>(a, Nt, tpw, st)   \
+                              : launch_fast_t<BITS, MT, GPT, ZM, kEpNone>(a, Nt, tpw, st)
+  if (group % kTileK == 0) QLIN_FE(1);
+  if (group == 64) QLIN_FE(2);
+  QLIN_FE(4);
+#undef QLIN_FE
+}
+
 template <int BITS, int MT, int ZM>
 int launch_gemv_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st, const Ep& e) {
@@ -461,6 +668,16 @@ int launch_gemv_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
 template <int BITS, int ZM>
 int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st, const Ep& e) {
+  int W = 0, lw = 0, tpw = 0;
+  if (fast_ok(M, K, group, e) &&
+      fast_geometry((N + kTileN - 1) / kTileN, K / kTileK, W, lw, tpw)) {
+#define QLIN_F(MT) \
+  return launch_fast<BITS, MT, ZM>(qw, qsz, x, bias, y, M, N, K, group, W, lw, tpw, st, e)
+    if (M == 1) QLIN_F(1);
+    if (M == 2) QLIN_F(2);
+    QLIN_F(4);
+#undef QLIN_F
+  }
   if (M == 1) return launch_gemv_g<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   if (M == 2) return launch_gemv_g<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   if (M <= 4) return launch_gemv_g<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);

@@ -46,6 +46,7 @@ SIGNATURES = {
     "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
+    "qlin_gemm_block_cols": ([_l, _l, _i], _i),
     "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _i, _i, _p, _p],
                            _i),
     "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),

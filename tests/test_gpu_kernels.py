@@ -220,7 +220,7 @@ def test_gptq_checkpoint_conversion(bits, group):
     assert_close_to_ref(n(y), O.linear_ref(x, ref_w, tensors["lin.bias"].numpy()))
 
 
-def _pick_bn(M, N, cus=256):
+def _pick_bn(M, N, cus):
     """Mirror of qlin_gemm.hip pick_bn (block width by rounds of blocks over the CUs; 128 = the
     64 x 128 block for small grids)."""
     if -(-M // 128) * -(-N // 256) * 2 <= cus:
@@ -241,14 +241,41 @@ def _pick_bn(M, N, cus=256):
 @pytest.mark.parametrize("bits,group", [(4, 128), (4, 64), (3, 64), (2, 32)])
 def test_gemm_block_widths(bits, group, M, N, bn):
     """The 128 x 256 / 384 / 512 and 64 x 128 block tiles (pick_bn: whole rounds of blocks over
-    256 CUs) with ragged M and N; g64 / g32 take the wider tiles' checked k-step form."""
-    assert _pick_bn(M, N) == bn
+    the CUs) with ragged M and N; g64 / g32 take the wider tiles' checked k-step form.  The width
+    the library picks is read back through qlin_gemm_block_cols (the expected widths are those of
+    a 256-CU MI355X)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    picked = qlin.load_library().qlin_gemm_block_cols(M, N, bits)
+    assert picked == _pick_bn(M, N, cus)
+    if cus != 256:
+        pytest.skip(f"{cus} CUs: the {bn}-column block is not what this shape picks here")
+    assert picked == bn
     K = 1024
     qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=bits + group)
     x = rand_x(M, K, seed=7)
     y = n(qlin.gemm(t(x), qw, qsz, None, N, K, bits, group, fl))
     rows = np.unique(np.r_[0:64, M // 2 - 64:M // 2 + 64, M - 96:M].clip(0, M - 1))  # fp64 ref sample
     assert_close_to_ref(y[rows], O.linear_ref(x[rows], wdq), what=f"gemm bn{bn} b{bits} g{group}")
+
+
+@pytest.mark.parametrize("bits,group", [(4, 128), (3, 64), (2, 32)])
+def test_gemm_block_widths_bit_identical(bits, group):
+    """Every block width accumulates each output in the same k order: the first 128 rows of
+    launches that pick the 128 x 256 / 384 / 512 blocks equal, bit for bit, a 128-row launch that
+    picks the 64 x 128 block."""
+    lib = qlin.load_library()
+    K = 1024
+    seen = set()
+    for N, Ms in ((4096, (2048, 8192)), (4112, (4129,))):
+        qw, qsz, fl, _ = _packed(N, K, bits, group, seed=N + bits)
+        xb = t(rand_x(max(Ms), K, seed=11))
+        small = qlin.gemm(xb[:128].contiguous(), qw, qsz, None, N, K, bits, group, fl)
+        assert lib.qlin_gemm_block_cols(128, N, bits) == 128
+        for M in Ms:
+            seen.add(lib.qlin_gemm_block_cols(M, N, bits))
+            big = qlin.gemm(xb[:M].contiguous(), qw, qsz, None, N, K, bits, group, fl)
+            assert torch.equal(big[:128], small), f"M={M} N={N} b{bits} g{group}"
+    assert len(seen) >= 2, seen  # 256-CU MI355X: {256, 384, 512}
 
 
 @pytest.mark.parametrize("N", [8192 + 16 * 3 + 5, 8192 + 16])

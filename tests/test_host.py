@@ -62,6 +62,7 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert lib.qlin_pack_codes(None, 16, 64, 4, None, None) == 1
     assert lib.qlin_pack_codes(p, 16, 48, 4, p, None) == 1  # K % 32
     assert lib.qlin_pack_codes(p, 16, 64, 5, p, None) == 1  # bits
+    assert lib.qlin_gemm_block_cols(0, 16, 4) == -1 and lib.qlin_gemm_block_cols(16, 16, 5) == -1
     assert lib.qlin_error_string(1) == b"invalid argument"
 
 

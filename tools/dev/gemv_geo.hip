@@ -23,3 +23,24 @@ extern "C" int geo_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
 #undef G
   return (int)hipGetLastError();
 }
+
+// the decode fast path (gemv_fast_kernel) with an explicit geometry: W waves (power of two),
+// PF tiles in flight, LOOP = refill loop compiled in (required when ceil(Kt / W) > PF)
+extern "C" int geo_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, uint16_t* y,
+                        int N, int K, int W, int PF, int LOOP, void* stream) {
+  const int Nt = (N + kTileN - 1) / kTileN;
+  FastArgs a;
+  a.qw = qw; a.qsz = qsz; a.x = (const _Float16*)x; a.bias = nullptr; a.res = nullptr;
+  a.y = (_Float16*)y; a.M = 1; a.N = N; a.K = K; a.Kt = K / kTileK; a.G = K / 128;
+  int lw = 0;
+  while ((2 << lw) <= W) ++lw;
+  a.W = 1 << lw; a.lw = lw; a.cmagic = 1u << 31;
+  if ((a.Kt + a.W - 1) / a.W > PF && !LOOP) return 1;
+#define F(P, L) hipLaunchKernelGGL((gemv_fast_kernel<4, 1, 1, kZNarrow, kEpNone, P, L>), dim3(Nt), \
+                                   dim3(64 * a.W), 0, (hipStream_t)stream, a)
+  if (PF == 2) { if (LOOP) F(2, true); else F(2, false); }
+  else if (PF == 4) { if (LOOP) F(4, true); else F(4, false); }
+  else { if (LOOP) F(8, true); else F(8, false); }
+#undef F
+  return (int)hipGetLastError();
+}

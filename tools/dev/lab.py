@@ -74,6 +74,11 @@ CONFIGS = [  # (W, PF, NT, MODE, RED, XL)
     (16, 2, 1, 0, 1, 1), (16, 2, 1, 1, 1, 1), (16, 2, 1, 10, 1, 1), (8, 4, 1, 10, 1, 1),
     (8, 2, 1, 10, 1, 1), (16, 2, 1, 3, 1, 1),
 ]
+if os.environ.get("LAB_CONFIGS"):
+    CONFIGS = [tuple(int(v) for v in c.split(",")) for c in os.environ["LAB_CONFIGS"].split(";")]
+STAMP_CONFIGS = [(16, 2, 1, 10, 1, 1)]
+if os.environ.get("LAB_STAMPS"):
+    STAMP_CONFIGS = [tuple(int(v) for v in c.split(",")) for c in os.environ["LAB_STAMPS"].split(";")]
 res = {}
 res["stream"] = timed(lambda: [launch_stream(m) for m in mats])
 print(f"stream: {res['stream']:.3f} us", flush=True)
@@ -111,7 +116,7 @@ def ring_stamped(fn_stamped, fn):
 ring_stamped(lambda j, m: launch_stream(m, stamps), lambda j, m: launch_stream(m))
 torch.cuda.synchronize()
 show("stream (ring)", 2048)
-for c in ((16, 2, 1, 10, 1, 1),):
+for c in STAMP_CONFIGS:
     W, PF, NT, MODE, RED, XL = c
     stamps.zero_()
     ring_stamped(lambda j, m: launch(m, ys[j % 8], W, PF, NT, MODE, stamps, RED, XL),
