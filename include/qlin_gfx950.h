@@ -199,6 +199,28 @@ int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const
                      float scale_div, float* partials, int32_t* counters, void* stream);
 
 /*
+ * Fused prefill attention (many query tokens per sequence): the same attention core as
+ * qlin_attn_decode — repeat_kv, fp32 QK^T, / sqrt(head_dim) (as torch: x the fp32 reciprocal),
+ * + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV (models/int_llama_layer.py:137-165 of
+ * the reference, QuantMatMul qkt / pv of quant/int_matmul.py at A16) — as one kernel that keeps
+ * the [S, L] scores on chip (online softmax) and multiplies on the fp32 matrix cores; equal to the
+ * reference up to fp32 rounding (summation order), not bit for bit.
+ *   q    fp32 [B, Hq, S, D] (after RoPE);  k, v  fp16 [B, Hkv, L, D], L >= S: query row i sits at
+ *   key position L - S + i;  mask  [B', 1, S, L] additive, QLIN_F16 or QLIN_F32, batch b at
+ *   mask + b * mask_batch_stride elements (0: broadcast), or NULL (no masking);
+ *   causal != 0 (mask required): the caller guarantees mask[., i, j] <= -1e4 for every key
+ *   j > L - S + i, so key blocks past a query block's diagonal are skipped (their exp()
+ *   underflows to 0 in the reference as well);
+ *   out  [B, S, Hq, D] (the layer's transpose(1, 2) layout) in out_dtype: QLIN_F32, or QLIN_F16 =
+ *   the fp32 result rounded once (the layer's .to(fp16) before o_proj);  scale_div = sqrt(D).
+ *   D == 128, Hq / Hkv in {1, 2, 4, 8}.
+ */
+int qlin_attn_prefill(const float* q, const uint16_t* k, const uint16_t* v, const void* mask,
+                      int mask_dtype, int64_t mask_batch_stride, int causal, void* out,
+                      int out_dtype, int64_t B, int Hq, int Hkv, int64_t S, int64_t L, int D,
+                      float scale_div, void* stream);
+
+/*
  * RMSNorm of the quantized LLaMA layer (OmniLlamaRMSNorm.forward, quant/omni_norm.py:52-63 of the
  * reference): y = (weight * (x * rsqrt(mean(x^2) + eps))).to(fp16), fp32 inside.
  *   x, y  fp16 [rows, H];  weight  fp32 [H] (the fp16 weight upcast: exact).

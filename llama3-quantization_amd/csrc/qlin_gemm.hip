@@ -149,7 +149,8 @@ __device__ __forceinline__ void read_a(h8 (&a)[MB], const unsigned char* as, int
 }
 
 // FULL: every k-tile lies inside K (K % 128 == 0, chosen per launch): straight-line k-steps
-template <int BITS, int WN_, int GPT, int ZM, bool FULL, int NW>
+// (ABL bit 2, lab only: the raw packed words stand in for the dequantized B fragment)
+template <int BITS, int WN_, int GPT, int ZM, bool FULL, int NW, int ABL = 0>
 __device__ __forceinline__ void compute_stage(const unsigned char* st, const GemmGeo& g, int kt,
                                               f4 (&acc)[Cfg<BITS, WN_, NW>::MB][Cfg<BITS, WN_, NW>::NB]) {
   using C = Cfg<BITS, WN_, NW>;
@@ -197,7 +198,11 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       uint32_t v[4];
-      dequant_step<BITS, ZM, S>(pc[nb], mg, gq[nb], v);
+      if constexpr (ABL & 4) {
+        v[0] = pc[nb].w[0]; v[1] = pc[nb].w[1 % BITS]; v[2] = pc[nb].w[2 % BITS]; v[3] = pc[nb].w[3 % BITS];
+      } else {
+        dequant_step<BITS, ZM, S>(pc[nb], mg, gq[nb], v);
+      }
       const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
@@ -211,7 +216,7 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
 }
 
 // ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
-// the DMA after the first k-tile; the library instantiates ABL = 0 only
+// the DMA after the first k-tile, bit 2 the dequant VALU; the library instantiates ABL = 0 only
 template <int BITS, int WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
@@ -255,7 +260,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
     if (!(ABL & 2) && kt + 1 < g.Kt)
       load_stage<BITS, WN_, GPT, NW>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
     if (!(ABL & 1))
-      compute_stage<BITS, WN_, GPT, ZM, KFULL, NW>(smem + (kt & 1) * C::STAGE, g, kt, acc);
+      compute_stage<BITS, WN_, GPT, ZM, KFULL, NW, ABL>(smem + (kt & 1) * C::STAGE, g, kt, acc);
   }
 
   // epilogue: lane (n, q) holds C[4q + i][n] of each 16 x 16 block

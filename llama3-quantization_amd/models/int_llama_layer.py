@@ -167,13 +167,17 @@ class QuantLlamaAttention(nn.Module):
         self.qkv = None  # FusedPackedLinear after fuse_packed()
         self.decode_kernel = False  # qlin_attn_decode for one-token steps (fuse_packed turns it on)
         self.rope_kernel = False  # qlin_rope_f16 (fuse_packed turns it on)
+        self.prefill_kernel = False  # qlin_attn_prefill for multi-token windows (opt-in)
 
-    def fuse_packed(self):
+    def fuse_packed(self, prefill_attention: bool = False):
         """q_proj + k_proj + v_proj as one fused packed launch (all read the normed hidden), and
-        the fused decode-attention kernel for one-token steps."""
+        the fused decode-attention kernel for one-token steps; ``prefill_attention`` also routes
+        multi-token windows through the fused prefill-attention kernel (fp32, online softmax:
+        equal to the reference attention to fp32 rounding instead of bit for bit)."""
         self.qkv = FusedPackedLinear([self.q_proj, self.k_proj, self.v_proj])
         self.decode_kernel = True
         self.rope_kernel = hasattr(self.rotary_emb, "cos_cached")
+        self.prefill_kernel = bool(prefill_attention)
         return self
 
     def _attn_bypassed(self):
@@ -259,6 +263,18 @@ class QuantLlamaAttention(nn.Module):
                                            out_dtype=act_dtype if act_dtype == torch.float16
                                            else torch.float32)
             attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
+            return self._out(attn_output, residual), None, past_key_value
+
+        if (self.prefill_kernel and q_len > 1 and not output_attentions and self._attn_bypassed()
+                and qlin.attn_prefill_supported(query_states, key_states, attention_mask)):
+            # fused prefill attention: repeat_kv, QK^T, / sqrt(d), + mask, clamp, softmax and PV
+            # in one kernel (fp32 matrix cores, online softmax), output already in the
+            # transpose(1, 2) layout and, for fp16 activations, rounded once to fp16
+            attn_output = qlin.attn_prefill(query_states, key_states, value_states, attention_mask,
+                                            math.sqrt(self.head_dim),
+                                            out_dtype=act_dtype if act_dtype == torch.float16
+                                            else torch.float32)
+            attn_output = attn_output.reshape(bsz, q_len, self.hidden_size).to(act_dtype)
             return self._out(attn_output, residual), None, past_key_value
 
         key_states = repeat_kv(key_states, self.num_key_value_groups)
@@ -369,10 +385,11 @@ class QuantLlamaDecoderLayer(nn.Module):
             if isinstance(m, (QuantLinear, QuantMatMul)):
                 m.set_quant_state(weight_quant, act_quant)
 
-    def fuse_packed_projections(self):
+    def fuse_packed_projections(self, prefill_attention: bool = False):
         """After packing: q/k/v and gate/up (+ SiLU·mul) each become one fused launch, and the two
-        residual adds move into the o_proj / down_proj epilogues."""
-        self.self_attn.fuse_packed()
+        residual adds move into the o_proj / down_proj epilogues (SURVEY.md §8 f4);
+        ``prefill_attention``: multi-token windows also take the fused prefill-attention kernel."""
+        self.self_attn.fuse_packed(prefill_attention)
         self.mlp.fuse_packed()
         self.fused_epilogues = self.self_attn.o_proj.packed and self.mlp.down_proj.packed
         self.input_layernorm.use_kernel = True

@@ -53,6 +53,8 @@ SIGNATURES = {
     "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
     "qlin_attn_scores_f32": ([_p, _p, _i, _l, _l, _l, _l, _l, ctypes.c_float, _p], _i),
     "qlin_attn_decode_partials_bytes": ([_l, _i, _i, _l], _l),
+    "qlin_attn_prefill": ([_p, _p, _p, _p, _i, _l, _i, _p, _i, _l, _i, _i, _l, _l, _i,
+                           ctypes.c_float, _p], _i),
     "qlin_attn_decode": ([_p, _p, _p, _p, _p, _i, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p],
                          _i),
 }
@@ -498,4 +500,70 @@ def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32):
                               B, Hq, Hkv, L, D, float(scale_div), _ptr(part), _ptr(cnt),
                               _stream(q))
     _check(rc, "qlin_attn_decode")
+    return out
+
+
+def attn_prefill_supported(q, k, mask=None):
+    """Whether qlin_attn_prefill takes this call (see attn_prefill)."""
+    return (q.is_cuda and q.dim() == 4 and k.dim() == 4 and q.shape[-1] == ATTN_D
+            and q.dtype == torch.float32 and k.dtype == torch.float16
+            and q.shape[0] == k.shape[0] and q.shape[2] <= k.shape[2]
+            and q.shape[1] % k.shape[1] == 0 and q.shape[1] // k.shape[1] in (1, 2, 4, 8)
+            and (mask is None or (mask.dim() == 4 and mask.shape[1] == 1
+                                  and mask.shape[-2:] == (q.shape[2], k.shape[2])
+                                  and mask.shape[0] in (1, q.shape[0])
+                                  and mask.dtype in (torch.float16, torch.float32))))
+
+
+_CAUSAL = {}
+
+
+def mask_is_causal(mask, S, L) -> bool:
+    """The additive mask [B', 1, S, L] leaves every key past a query's diagonal (key > L - S + i)
+    at <= -1e4 (so its exp() underflows to 0) and keeps the diagonal itself open; cached per
+    tensor version (one check per forward, the decoder layers share the mask)."""
+    key = (mask.data_ptr(), mask._version, tuple(mask.shape), tuple(mask.stride()), mask.dtype)
+    hit = _CAUSAL.get(key)
+    if hit is not None:
+        return hit
+    i = torch.arange(S, device=mask.device)[:, None]
+    j = torch.arange(L, device=mask.device)[None, :]
+    above = j > (L - S) + i
+    m = mask[:, 0].float()
+    open_max = torch.where(above, torch.full_like(m, -float("inf")), m).amax(dim=-1)  # per row
+    ok = bool((m[:, above] <= -1e4).all()) and bool((open_max > -1e4).all())
+    if len(_CAUSAL) > 64:
+        _CAUSAL.clear()
+    _CAUSAL[key] = ok
+    return ok
+
+
+def attn_prefill(q, k, v, mask, scale_div, out_dtype=torch.float32):
+    """softmax(q k^T / scale_div + mask) v for a window of S query tokens: q fp32 [B, Hq, S, D]
+    (after RoPE), k/v fp16 [B, Hkv, L, D] (L >= S: a cached prefix precedes the window), mask
+    [B', 1, S, L] fp16/fp32 or None -> [B, S, Hq, D] (the layer's transposed layout) in out_dtype
+    (fp32, or the fp32 result rounded once to fp16)."""
+    if not attn_prefill_supported(q, k, mask):
+        raise ValueError("attn_prefill: unsupported shapes / dtypes")
+    if not (q.is_cuda and k.is_cuda and v.is_cuda):
+        raise RuntimeError("qlin kernels run on gfx950 only: got a CPU tensor")
+    B, Hq, S, D = q.shape
+    Hkv, L = k.shape[1], k.shape[2]
+    q = q.contiguous()
+    k = k.contiguous()
+    v = v.contiguous()
+    m, mdt, mbs, causal = None, F16, 0, 0
+    if mask is not None:
+        # batch-broadcast masks (expand()ed views, batch stride 0) are passed as they lie
+        m = mask
+        if m.stride(-1) != 1 or m.stride(-2) != L or (m.shape[0] > 1 and m.stride(0) not in (0, S * L)):
+            m = m.contiguous()
+        mdt = _dtcode(m)
+        mbs = m.stride(0) if m.shape[0] > 1 else 0
+        causal = int(mask_is_causal(m, S, L))
+    out = torch.empty(B, S, Hq, D, dtype=out_dtype, device=q.device)
+    rc = load_library().qlin_attn_prefill(_ptr(q), _ptr(k), _ptr(v), _ptr(m), mdt, mbs, causal,
+                                          _ptr(out), _dtcode(out), B, Hq, Hkv, S, L, D,
+                                          float(scale_div), _stream(q))
+    _check(rc, "qlin_attn_prefill")
     return out

@@ -108,3 +108,82 @@ def test_layer_decode_kernel_matches_torch_path():
         got = layer(x, attention_mask=mask, position_ids=pos, past_key_value=past)[0]
     rel = ((got.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
     assert rel < 2e-3, rel
+
+
+def _causal_mask(B, S, L, dtype=torch.float16, pad=None):
+    """HF-style additive 4D mask [B, 1, S, L]: query i (key position L - S + i) sees keys <= its
+    position; ``pad`` left-pads batch b's first pad[b] keys as well (non-causal pattern)."""
+    i = torch.arange(S, device="cuda")[:, None]
+    j = torch.arange(L, device="cuda")[None, :]
+    m = torch.zeros(B, 1, S, L, device="cuda", dtype=dtype)
+    m[:, 0][:, j.expand(S, L) > (L - S) + i.expand(S, L)] = torch.finfo(dtype).min
+    if pad is not None:
+        for b, p in enumerate(pad):
+            m[b, 0, :, :p] = torch.finfo(dtype).min
+    return m
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,S,L", [(1, 32, 8, 128, 128), (1, 32, 8, 257, 257),
+                                          (1, 8, 8, 100, 137), (2, 16, 4, 65, 65),
+                                          (1, 16, 2, 33, 100), (1, 8, 1, 200, 200),
+                                          (1, 4, 4, 1, 40), (1, 32, 8, 2048, 2048)])
+@pytest.mark.parametrize("mask_kind", ["causal", "causal_f32", "none"])
+def test_attn_prefill_matches_reference(B, Hq, Hkv, S, L, mask_kind):
+    """Fused prefill attention (qlin_attn_prefill, fp32 matrix cores, online softmax) vs the
+    reference formulation in float64; causal masks take the block-skipping path."""
+    g = torch.Generator(device="cuda").manual_seed(B * 7919 + S * 31 + L)
+    q = torch.randn(B, Hq, S, 128, device="cuda", generator=g) * 0.5
+    k = torch.randn(B, Hkv, L, 128, device="cuda", generator=g).half()
+    v = torch.randn(B, Hkv, L, 128, device="cuda", generator=g).half()
+    mask = None
+    if mask_kind != "none":
+        mask = _causal_mask(B, S, L, torch.float32 if mask_kind == "causal_f32" else torch.float16)
+        assert qlin.mask_is_causal(mask, S, L)
+    out = qlin.attn_prefill(q, k, v, mask, math.sqrt(128))
+    ref = _ref(q, k, v, mask).transpose(1, 2)
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 1e-5 * max(1.0, ref.abs().max().item()), err
+    out16 = qlin.attn_prefill(q, k, v, mask, math.sqrt(128), out_dtype=torch.float16)
+    assert out16.dtype == torch.float16 and torch.equal(out16, out.half())
+
+
+def test_attn_prefill_padding_mask_is_not_causal():
+    """Left padding on top of the causal pattern keeps every key block (non-causal path), and a
+    fully masked padded query row reproduces the reference's softmax over finfo.min scores."""
+    B, Hq, Hkv, S = 2, 8, 2, 150
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q = torch.randn(B, Hq, S, 128, device="cuda", generator=g)
+    k = torch.randn(B, Hkv, S, 128, device="cuda", generator=g).half()
+    v = torch.randn(B, Hkv, S, 128, device="cuda", generator=g).half()
+    mask = _causal_mask(B, S, S, pad=[0, 70])
+    assert not qlin.mask_is_causal(mask, S, S)
+    out = qlin.attn_prefill(q, k, v, mask, math.sqrt(128))
+    ref = _ref(q, k, v, mask).transpose(1, 2)
+    # rows 0..69 of batch 1 see no open key: their scores are qk / sqrt(d) - 65504 quantised to
+    # the fp32 grid there (~0.004), so the kernel and an fp32 reference agree only loosely
+    live = torch.ones(B, S, dtype=torch.bool, device="cuda")
+    live[1, :70] = False
+    d = (out.double() - ref).abs().amax(dim=(2, 3))
+    assert d[live].max().item() <= 1e-5 * ref.abs().max().item()
+    assert d[~live].max().item() <= 2e-2 * ref.abs().max().item()
+    # a causal-looking mask that is broadcast over the batch
+    mask1 = _causal_mask(1, S, S)
+    out = qlin.attn_prefill(q, k, v, mask1, math.sqrt(128))
+    ref = _ref(q, k, v, mask1).transpose(1, 2)
+    assert (out.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_attn_prefill_rejects_unsupported():
+    q = torch.randn(1, 32, 8, 64, device="cuda")
+    k = torch.randn(1, 8, 8, 64, device="cuda").half()
+    assert not qlin.attn_prefill_supported(q, k)
+    q = torch.randn(1, 32, 9, 128, device="cuda")
+    k = torch.randn(1, 8, 8, 128, device="cuda").half()  # L < S
+    assert not qlin.attn_prefill_supported(q, k)
+    with pytest.raises(ValueError):
+        qlin.attn_prefill(q, k, k, None, 8.0)
+    lib = qlin.load_library()
+    p = 16
+    # causal without a mask, odd group size
+    assert lib.qlin_attn_prefill(p, p, p, None, 0, 0, 1, p, 0, 1, 8, 8, 4, 4, 128, 11.3, None) == 1
+    assert lib.qlin_attn_prefill(p, p, p, None, 0, 0, 0, p, 0, 1, 24, 8, 4, 4, 128, 11.3, None) == 1

@@ -11,6 +11,7 @@ pytestmark = pytest.mark.gpu
 
 from models.quant_llama import (build_random_quant_llama, eval_ppl, quant_args,  # noqa: E402
                                 rtn_quantize_)
+from quant import qlin  # noqa: E402
 from quant.int_linear import QuantLinear  # noqa: E402
 from quant.utils import pack_quant_linears  # noqa: E402
 
@@ -105,3 +106,41 @@ def test_fused_layer_w4a8_matches_unfused():
         got = [model(x) for x in toks]
     for a, b in zip(got, ref):
         assert _rel(a, b) < 1e-3, _rel(a, b)
+
+
+def test_fused_prefill_attention_matches_reference_attention():
+    """fuse_packed_projections(prefill_attention=True): multi-token windows take the fused
+    prefill-attention kernel (causal mask verified on the host, key blocks past the diagonal
+    skipped) — logits within 1e-3 relative of the reference attention path, and the PPL within
+    1e-4 relative."""
+    from transformers import LlamaConfig
+    cfg = LlamaConfig(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
+                      num_key_value_heads=2, num_hidden_layers=2, vocab_size=1000,
+                      max_position_embeddings=256, rms_norm_eps=1e-5, rope_theta=500000.0)
+    model = build_random_quant_llama(cfg, quant_args(4, 128), seed=15, device="cuda",
+                                     dtype=torch.float16)
+    rtn_quantize_(model, pack=True)
+    g = torch.Generator(device="cuda").manual_seed(8)
+    toks = [torch.randint(0, cfg.vocab_size, (1, T), device="cuda", generator=g)
+            for T in (2, 70, 200)]
+    testenc = torch.randint(0, cfg.vocab_size, (1, 4 * 64), device="cuda", generator=g)
+    with torch.no_grad():
+        for layer in model.layers:
+            layer.fuse_packed_projections()
+        ref = [model(x) for x in toks]
+        ppl_ref = eval_ppl(model, testenc, seqlen=64)
+        for layer in model.layers:
+            layer.fuse_packed_projections(prefill_attention=True)
+        assert model.layers[0].self_attn.prefill_kernel
+        calls = []
+        orig = qlin.attn_prefill
+        qlin.attn_prefill = lambda *a, **k: calls.append(1) or orig(*a, **k)
+        try:
+            got = [model(x) for x in toks]
+        finally:
+            qlin.attn_prefill = orig
+        assert len(calls) == 2 * len(toks)  # every layer of every window took the kernel
+        ppl = eval_ppl(model, testenc, seqlen=64)
+    for a, b in zip(got, ref):
+        assert _rel(a, b) < 1e-3, _rel(a, b)
+    assert abs(ppl - ppl_ref) / ppl_ref < 1e-4, (ppl, ppl_ref)

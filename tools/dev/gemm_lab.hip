@@ -37,6 +37,19 @@ extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
   return (int)hipGetLastError();
 }
 
+// the product's 8-wave 128 x BN block with the dequant VALU skipped (ABL bit 2) or not
+extern "C" int lab_gemm_nodq(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, uint16_t* y,
+                             int64_t M, int N, int K, int bn, int nodq, void* stream) {
+  const int tn = (N + bn - 1) / bn, tm = (int)((M + 127) / 128);
+#define L(B, A) hipLaunchKernelGGL((gemm_kernel<4, B, 1, kZNarrow, true, A, 8>), dim3(tm * tn), dim3(512), \
+                                   0, (hipStream_t)stream, qw, qsz, (const _Float16*)x, nullptr,         \
+                                   (_Float16*)y, M, N, K, 128, group_magic(128), tm, tn, nullptr, 0)
+  if (bn == 512) { if (nodq) L(512, 4); else L(512, 0); }
+  else { if (nodq) L(256, 4); else L(256, 0); }
+#undef L
+  return (int)hipGetLastError();
+}
+
 // the lab library does not link the GEMV or the quantizer: the skinny / act-quant branches of
 // qlin_linear_*_f16 are never taken here
 int qlin::gemv_ep(const uint32_t*, const uint32_t*, int, const uint16_t*, const uint16_t*,

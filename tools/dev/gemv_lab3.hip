@@ -13,6 +13,8 @@
 //   V 11: V 0 with the dequant + MFMA of both tiles run 3 times (a rolled loop: same code,
 //         warm instruction cache, data already in registers for passes 2 and 3)
 //   V 12: V 6 (loads only) with ~1000 bytes of never-executed code between its instructions
+//   V 13: V 0 with the block's whole x row staged in LDS once (one 16-B load per thread of waves
+//         0-7, one barrier) instead of one x load + LDS park per tile
 #include "../../llama3-quantization_amd/csrc/qlin_common.h"
 #include <type_traits>
 using namespace qlin;
@@ -22,11 +24,12 @@ __global__ __launch_bounds__(1024) void lab3(const uint32_t* __restrict__ qw,
                                              const uint32_t* __restrict__ qsz,
                                              const _Float16* __restrict__ x,
                                              _Float16* __restrict__ y, int N, int K) {
-  constexpr int V = V0 == 7 || V0 == 10 || V0 == 11 ? 0 : V0 == 8 ? 5 : V0 == 9 || V0 == 12 ? 6 : V0;
-  constexpr bool PRIO = V0 >= 7;
+  constexpr int V = V0 == 7 || V0 == 10 || V0 == 11 || V0 == 13 ? 0 : V0 == 8 ? 5 : V0 == 9 || V0 == 12 ? 6 : V0;
+  constexpr bool PRIO = V0 >= 7 && V0 <= 12;
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
   __shared__ __attribute__((aligned(16))) float red[16 * 16];
   __shared__ __attribute__((aligned(16))) uint32_t xs[16][2][64];
+  __shared__ __attribute__((aligned(16))) _Float16 xall[4096];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
@@ -43,7 +46,12 @@ __global__ __launch_bounds__(1024) void lab3(const uint32_t* __restrict__ qw,
         reinterpret_cast<const u4v*>(qw + (t0 + kt[u]) * 256 + lane * 4));
     pc[u].w[0] = v.x; pc[u].w[1] = v.y; pc[u].w[2] = v.z; pc[u].w[3] = v.w;
   }
-  if constexpr (V == 0) {
+  if constexpr (V0 == 13) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) sz[u] = qsz[(t0 + kt[u]) * 16 + n_in];
+    if (tid < 512) reinterpret_cast<uint4*>(xall)[tid] = reinterpret_cast<const uint4*>(x)[tid];
+    __syncthreads();
+  } else if constexpr (V == 0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       sz[u] = qsz[(t0 + kt[u]) * 16 + n_in];
@@ -83,11 +91,17 @@ __global__ __launch_bounds__(1024) void lab3(const uint32_t* __restrict__ qw,
     if constexpr (V0 == 10) {
       if (u == 1) __builtin_amdgcn_s_setprio(1);
     }
-    if constexpr (V == 0) xs[wave][u][lane] = xr[u];
     h8 xa[4];
-    const uint4* b = reinterpret_cast<const uint4*>(&xs[wave][u][0]);
+    if constexpr (V0 == 13) {
+      const uint4* b = reinterpret_cast<const uint4*>(xall + kt[u] * 128);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, b[4 * s + (lane >> 4)]);
+      for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, b[4 * s + (lane >> 4)]);
+    } else {
+      if constexpr (V == 0) xs[wave][u][lane] = xr[u];
+      const uint4* b = reinterpret_cast<const uint4*>(&xs[wave][u][0]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, b[4 * s + (lane >> 4)]);
+    }
     if constexpr (V == 6) {
       xo ^= pc[u].w[0] ^ pc[u].w[1] ^ pc[u].w[2] ^ pc[u].w[3] ^ sz[u];
       xo ^= __builtin_bit_cast(uint4, xa[0]).x ^ __builtin_bit_cast(uint4, xa[3]).y;
@@ -199,7 +213,8 @@ extern "C" int lab3_launch(const void* qw, const void* qsz, const void* x, void*
     case 9: L(9); break;
     case 10: L(10); break;
     case 11: L(11); break;
-    default: L(12); break;
+    case 12: L(12); break;
+    default: L(13); break;
   }
 #undef L
   return (int)hipGetLastError();

@@ -8,7 +8,8 @@ heads, vocab 128,256) and the "text" is seeded random tokens.  RTN int4 g128 exa
 omniquant() with epochs == 0, then:
   fake-quant: the reference's eval path (weight = W_dq, dense fp16 F.linear);
   packed:     the same layers after pack_quant_linears (gfx950 dequant-GEMM kernels), optionally
-              with fused q/k/v + gate/up launches.
+              with fused q/k/v + gate/up launches, and then also the fused prefill-attention
+              kernel (fp32, online softmax: equal to the reference attention to fp32 rounding).
 Reports PPL of both, their relative delta, the max relative logit difference on the first
 window, and ms per 2048-token window (HIP events, after one warm-up window).  Prints one JSON line.
 """
@@ -80,6 +81,9 @@ def main():
     for layer in model.layers:
         layer.fuse_packed_projections()
     ppl_fu, lg_fu, ms_fu = run("packed + fused projections")
+    for layer in model.layers:
+        layer.fuse_packed_projections(prefill_attention=True)
+    ppl_fa, lg_fa, ms_fa = run("packed + fused projections + fused prefill attention")
     rel = lambda x, y: ((x.double() - y.double()).abs().max() / y.double().abs().max()).item()
     out = {
         "what": "LLaMA3-8B-architecture (random init) PPL parity, packed vs fake-quant",
@@ -93,6 +97,10 @@ def main():
         "logits_rel_err_fused": rel(lg_fu, lg_fq),
         "ms_per_window_fake_quant": round(ms_fq, 2), "ms_per_window_packed": round(ms_pk, 2),
         "ms_per_window_packed_fused": round(ms_fu, 2),
+        "ppl_packed_fused_attn": ppl_fa,
+        "ppl_rel_delta_fused_attn": abs(ppl_fa - ppl_fq) / ppl_fq,
+        "logits_rel_err_fused_attn": rel(lg_fa, lg_fq),
+        "ms_per_window_packed_fused_attn": round(ms_fa, 2),
     }
     print(json.dumps(out), flush=True)
 
