@@ -208,9 +208,11 @@ int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const
  *   q    fp32 [B, Hq, S, D] (after RoPE);  k, v  fp16 [B, Hkv, L, D], L >= S: query row i sits at
  *   key position L - S + i;  mask  [B', 1, S, L] additive, QLIN_F16 or QLIN_F32, batch b at
  *   mask + b * mask_batch_stride elements (0: broadcast), or NULL (no masking);
- *   causal != 0 (mask required): the caller guarantees mask[., i, j] <= -1e4 for every key
+ *   causal = 1 (mask required): the caller guarantees mask[., i, j] <= -1e4 for every key
  *   j > L - S + i, so key blocks past a query block's diagonal are skipped (their exp()
- *   underflows to 0 in the reference as well);
+ *   underflows to 0 in the reference as well); causal = 2: the mask is exactly that pattern
+ *   (0 for j <= L - S + i, <= -1e4 above): it is applied arithmetically and never read (mask may
+ *   be NULL); causal = 0: the mask (if any) is read everywhere and no key block is skipped;
  *   out  [B, S, Hq, D] (the layer's transpose(1, 2) layout) in out_dtype: QLIN_F32, or QLIN_F16 =
  *   the fp32 result rounded once (the layer's .to(fp16) before o_proj);  scale_div = sqrt(D).
  *   D == 128, Hq / Hkv in {1, 2, 4, 8}.

@@ -20,19 +20,21 @@
 //
 // Decomposition: a 256-thread block = 4 waves = (hw query heads of one KV head) x (4 / hw 16-row
 // query sub-blocks), hw = min(Hq / Hkv, 4), so each staged K / V block serves hw heads (GQA: K / V
-// are read once per KV head, never expanded).  Per 64-key block: K [64][128] and V^T [128][64]
-// (fp16) are staged in LDS by all 256 threads, every wave computes its 16 x 64 score tile (32
-// MFMAs over d), the online softmax in registers (row reductions over the 16 lanes of a row by
-// DPP), parks P in its LDS slot (the C fragment's row / column roles are the A operand's
-// transposed) and accumulates O += P V (32 MFMAs).  The next block's K / V rows and mask tile are
-// fetched into registers while a block computes.  Lane (n, j) of an MFMA holds A[n][8j ..],
-// B[8j ..][n] and C rows 4j + e, column n — the scores and the output share the row layout, so
-// the rescale factors stay in registers.
+// are read once per KV head, never expanded).  Per 64-key block: K and V [64 keys][128 d] (fp16,
+// row-major, coalesced) are staged in LDS by all 256 threads; every wave computes the swapped
+// score tile S^T = K Q^T (16 keys x 16 rows per MFMA block, 32 MFMAs over d), so each lane holds
+// 16 scores of ONE query row (lane (n, j): row n, keys 16 sb + 4 j + e) — the online softmax
+// needs two cross-group shuffles per row statistic and P never leaves the registers: the S^T
+// fragments of two sub-blocks are, as they stand, the P^T operand of O^T = V^T P^T for a 32-key
+// step whose keys run in the order 4 j + e, 16 + 4 j + e; V^T comes from the row-major V tile by
+// ds_read_b64_tr_b16 (hardware transpose read) in that same key order (32 MFMAs).  The next
+// block's K / V rows and mask values are fetched into registers while a block computes.
 //
 // Causal windows (mask verified causal on the host): key blocks past a query block's last
 // diagonal position are skipped — their mask entries are <= -1e4, so exp() underflows to exactly
-// 0 in the reference too.  Query row i sits at key position L - S + i (a cached prefix of L - S
-// keys precedes the window).
+// 0 in the reference too; a mask that is exactly the causal pattern (0 on and below the diagonal)
+// is not read at all.  Query row i sits at key position L - S + i (a cached prefix of L - S keys
+// precedes the window).
 #include "qlin_common.h"
 #include "../../include/qlin_gfx950.h"
 
@@ -41,8 +43,7 @@ namespace {
 constexpr int kD = 128;       // head_dim
 constexpr int kKB = 64;       // keys per block
 constexpr int kKS = kD + 8;   // K row stride in LDS (halves): 272 B, conflict-free row reads
-constexpr int kVS = kKB + 8;  // V^T row stride (halves): 144 B
-constexpr int kPS = kKB + 4;  // P row stride (floats): 272 B
+constexpr int kVS = kD + 16;  // V row stride (halves): 288 B, conflict-free transposed reads
 constexpr int kMaxG = 8;      // query heads per KV head
 
 struct PrefillArgs {
@@ -83,10 +84,24 @@ __device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
   lo = (_Float16)(x - (float)hi);
 }
 
+typedef __fp16 tr4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+typedef __attribute__((address_space(3))) tr4* lds_tr4;
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q + p addresses row q, columns 4p .. 4p + 3 of a
+// 4 x 16 block of 16-bit elements; lane i receives column i of the 4 rows (row q in element q)
+__device__ __forceinline__ uint2 tr_read(const _Float16* p) {
+  const tr4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_tr4)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ float xshfl16(float v) { return __shfl_xor(v, 16); }
+__device__ __forceinline__ float xshfl32(float v) { return __shfl_xor(v, 32); }
+
+// GMASK: the mask values are read (any mask but the pure causal pattern)
+template <bool GMASK>
 __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) {
-  __shared__ __attribute__((aligned(16))) _Float16 ks[kKB * kKS];   // 17,408 B
-  __shared__ __attribute__((aligned(16))) _Float16 vt[kD * kVS];    // 18,432 B
-  __shared__ __attribute__((aligned(16))) float ps[4][16 * kPS];    // 17,408 B
+  __shared__ __attribute__((aligned(16))) _Float16 ks[kKB * kKS];  // K [64 keys][128 d], 17,408 B
+  __shared__ __attribute__((aligned(16))) _Float16 vs[kKB * kVS];  // V [64 keys][128 d], 18,432 B
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -106,6 +121,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   const int row0 = rb * RB + (wave >> a.lhw) * 16;  // the wave's first query row
   const int L = a.L, S = a.S, off = L - S;         // query row i <-> key position off + i
   const bool wave_rows = row0 < S;                 // wave-uniform
+  const int row = row0 + n;                        // this lane's query row (S^T: rows on lanes)
 
   // the block's key range and the wave's own (causal: up to the last row's diagonal)
   int kend = L, kend_w = L;
@@ -115,94 +131,85 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   }
   const int nkb = (kend + kKB - 1) / kKB;
 
-  // q as fp16 pairs in the A-operand layout of v_mfma_f32_16x16x32_f16: lane (n, j), d-step t
-  // holds q[row0 + n][32 t + 8 j .. + 7]
+  // q as fp16 pairs, the B operand of S^T = K Q^T: lane (n, j), d-step t holds
+  // q[row0 + n][32 t + 8 j .. + 7]
   qlin::h8 qh[4], ql[4];
   {
-    const float* qp = a.q + (((int64_t)b * a.Hq + hq) * S + min(row0 + n, S - 1)) * kD + 8 * j;
+    const float* qp = a.q + (((int64_t)b * a.Hq + hq) * S + min(row, S - 1)) * kD + 8 * j;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float4 x0 = reinterpret_cast<const float4*>(qp + 32 * t)[0];
-      const float4 x1 = reinterpret_cast<const float4*>(qp + 32 * t)[1];
-      const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      const f4v x0 = reinterpret_cast<const f4v*>(qp + 32 * t)[0];
+      const f4v x1 = reinterpret_cast<const f4v*>(qp + 32 * t)[1];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         _Float16 h, l;
-        split16(xv[e], h, l);
+        split16(e < 4 ? x0[e] : x1[e - 4], h, l);
         qh[t][e] = h;
         ql[t][e] = l;
       }
     }
   }
+  // O^T accumulators: lane (n, j), d block c holds O[row][16 c + 4 j + e]
   f4v o[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) o[c] = f4v{0.f, 0.f, 0.f, 0.f};
-  float m[4], l[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) { m[e] = -INFINITY; l[e] = 0.f; }
+  float m = -INFINITY, l = 0.f;  // running max / sum of the lane's row
 
   const _Float16* kbase = a.k + ((int64_t)b * a.Hkv + hkv) * L * kD;
   const _Float16* vbase = a.v + ((int64_t)b * a.Hkv + hkv) * L * kD;
   const char* mrow = nullptr;
-  if (a.mask) {
+  if constexpr (GMASK) {
     const int64_t esz = a.mask_f32 ? 4 : 2;
-    mrow = reinterpret_cast<const char*>(a.mask) + (int64_t)b * a.mask_bs * esz;
+    mrow = reinterpret_cast<const char*>(a.mask) + ((int64_t)b * a.mask_bs +
+                                                    (int64_t)min(row, S - 1) * L) * esz;
   }
-  float* pw = ps[wave];
 
-  // next block's K / V rows and the wave's mask tile, in registers while this block computes
+  // the next block's K / V rows (and the lane's mask values), in registers while a block computes
   u4v kr[4], vr[4];
   float mk[4][4];
   auto fetch = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // K: chunk c = tid + 256 u -> key c / 16, d 8 (c % 16)
+    for (int u = 0; u < 4; ++u) {  // chunk c = tid + 256 u -> key c / 16, d 8 (c % 16)
       const int c = tid + 256 * u, key = c >> 4, d8 = (c & 15) * 8;
-      kr[u] = *reinterpret_cast<const u4v*>(kbase + (int64_t)min(k0 + key, L - 1) * kD + d8);
+      const int64_t r = (int64_t)min(k0 + key, L - 1) * kD + d8;
+      kr[u] = *reinterpret_cast<const u4v*>(kbase + r);
+      vr[u] = *reinterpret_cast<const u4v*>(vbase + r);
     }
+    if constexpr (GMASK) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)  // V: lane = key, d 8 (wave + 4 u)
-      vr[u] = *reinterpret_cast<const u4v*>(vbase + (int64_t)min(k0 + lane, L - 1) * kD +
-                                             (wave + 4 * u) * 8);
+      for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
-    for (int sb = 0; sb < 4; ++sb)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        mk[sb][e] = 0.f;
-        if (mrow) {
-          const int64_t idx =
-              (int64_t)min(row0 + 4 * j + e, S - 1) * L + min(k0 + 16 * sb + n, L - 1);
-          mk[sb][e] = a.mask_f32 ? reinterpret_cast<const float*>(mrow)[idx]
-                                 : (float)reinterpret_cast<const _Float16*>(mrow)[idx];
+        for (int e = 0; e < 4; ++e) {
+          const int kk = min(k0 + 16 * sb + 4 * j + e, L - 1);
+          mk[sb][e] = a.mask_f32 ? reinterpret_cast<const float*>(mrow)[kk]
+                                 : (float)reinterpret_cast<const _Float16*>(mrow)[kk];
         }
-      }
+    }
   };
   fetch(0);
 
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * kKB;
-    __syncthreads();  // every wave is done with the previous block's K / V^T
+    __syncthreads();  // every wave is done with the previous block's K / V
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = tid + 256 * u, key = c >> 4, d8 = (c & 15) * 8;
       *reinterpret_cast<u4v*>(ks + key * kKS + d8) = kr[u];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {  // V^T: each instruction writes 64 consecutive keys of 8 rows
-      const int d8 = (wave + 4 * u) * 8;
-      const qlin::h8 h = __builtin_bit_cast(qlin::h8, vr[u]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) vt[(d8 + e) * kVS + lane] = h[e];
+      *reinterpret_cast<u4v*>(vs + key * kVS + d8) = vr[u];
     }
     float mc[4][4];
+    if constexpr (GMASK) {
 #pragma unroll
-    for (int sb = 0; sb < 4; ++sb)
+      for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) mc[sb][e] = mk[sb][e];
+        for (int e = 0; e < 4; ++e) mc[sb][e] = mk[sb][e];
+    }
     __syncthreads();
     fetch(k0 + kKB);  // lands while this block computes (past the last block: clamped, unused)
     if (!wave_rows || k0 >= kend_w) continue;  // wave-uniform; the wave still stages and syncs
 
-    // scores S = Q K^T (fp32 accumulate of q_hi k + q_lo k): C rows 4 j + e, key 16 sb + n
+    // S^T = K Q^T (fp32 accumulate of k q_hi + k q_lo): lane (n, j) of sub-block sb holds
+    // S[row][k0 + 16 sb + 4 j + e]
     f4v sc[4];
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) sc[sb] = f4v{0.f, 0.f, 0.f, 0.f};
@@ -211,93 +218,88 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
 #pragma unroll
       for (int sb = 0; sb < 4; ++sb) {
         const qlin::h8 kf = *reinterpret_cast<const qlin::h8*>(ks + (16 * sb + n) * kKS + 32 * t + 8 * j);
-        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[t], kf, sc[sb], 0, 0, 0);
-        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql[t], kf, sc[sb], 0, 0, 0);
+        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[t], sc[sb], 0, 0, 0);
+        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[t], sc[sb], 0, 0, 0);
       }
-    // scale, mask, clamp (the reference's order), keys past L masked out
-    float mloc[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-    for (int sb = 0; sb < 4; ++sb) {
-      const bool kin = k0 + 16 * sb + n < L;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma clang fp contract(off)
-        float sv = sc[sb][e] * a.inv;
-        if (mrow) {
-          sv = sv + mc[sb][e];
-          sv = (sv != sv) ? sv : fmaxf(sv, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
-        }
-        sv = kin ? sv : -INFINITY;
-        sc[sb][e] = sv;
-        mloc[e] = fmaxf(mloc[e], sv);
-      }
-    }
-    // online softmax: row max over the 64 keys, rescale, P = exp(s - m)
-    float alpha[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float mb = row16_max(mloc[e]);
-      const float mn = fmaxf(m[e], mb);
-      alpha[e] = (mn == -INFINITY) ? 1.f : expf(m[e] - mn);
-      m[e] = mn;
-      float rs = 0.f;
-#pragma unroll
-      for (int sb = 0; sb < 4; ++sb) {
-        const float pv = (mn == -INFINITY) ? 0.f : expf(sc[sb][e] - mn);
-        sc[sb][e] = pv;
-        rs += pv;
-      }
-      l[e] = l[e] * alpha[e] + qlin::row16_sum(rs);
-    }
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[c][e] *= alpha[e];
-    // park P x 2^12 (P <= 1: its fp16 pair stays out of the subnormals down to 2^-26) as
-    // P[row][key], rows 4 j + e, key 16 sb + n; lane (n, j) of key step t reads P[n][32 t + 8 j ..]
+    // scale, mask, clamp (the reference's order); keys past L, and in the pure causal pattern keys
+    // past the row's diagonal, drop out (-inf: exp() gives the reference's exact 0)
+    float mloc = -INFINITY;
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) pw[(4 * j + e) * kPS + 16 * sb + n] = sc[sb][e] * 4096.f;
-    // O += P V (fp32 accumulate of p_hi v + p_lo v): d block c, lane (n, j) of key step t takes
-    // V[32 t + 8 j ..][16 c + n] = V^T[16 c + n][32 t + 8 j ..]
+      for (int e = 0; e < 4; ++e) {
+#pragma clang fp contract(off)
+        const int kk = k0 + 16 * sb + 4 * j + e;
+        float sv = sc[sb][e] * a.inv;
+        if constexpr (GMASK) {
+          sv = sv + mc[sb][e];
+          sv = (sv != sv) ? sv : fmaxf(sv, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
+        }
+        const bool open = kk < L && (a.causal != 2 || kk <= off + row);
+        sv = open ? sv : -INFINITY;
+        sc[sb][e] = sv;
+        mloc = fmaxf(mloc, sv);
+      }
+    // online softmax over the row's 64 keys (its 16 values on this lane, x 4 lane groups)
+    mloc = fmaxf(mloc, xshfl16(mloc));
+    mloc = fmaxf(mloc, xshfl32(mloc));
+    const float mn = fmaxf(m, mloc);
+    const float alpha = (mn == -INFINITY) ? 1.f : expf(m - mn);
+    m = mn;
+    float rs = 0.f;
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = (mn == -INFINITY) ? 0.f : expf(sc[sb][e] - mn);
+        sc[sb][e] = pv * 4096.f;  // x 2^12: the fp16 pair of a small P stays out of the subnormals
+        rs += pv;
+      }
+    rs += xshfl16(rs);
+    rs += xshfl32(rs);
+    l = l * alpha + rs;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o[c] *= alpha;
+    // O^T += V^T P^T: key step t (32 keys) in slot order 32 t + 4 j + e, then 32 t + 16 + 4 j + e —
+    // P^T is the S^T fragments of sub-blocks 2t, 2t + 1 as they stand; V^T by transposed reads of
+    // the row-major V tile (lane 4 q + p of group j: key 32 t [+ 16] + 4 j + q, d 16 c + 4 p)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       qlin::h8 ph, pl;
-      {
-        const float4 p0 = reinterpret_cast<const float4*>(pw + n * kPS + 32 * t + 8 * j)[0];
-        const float4 p1 = reinterpret_cast<const float4*>(pw + n * kPS + 32 * t + 8 * j)[1];
-        const float pvv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          _Float16 h, lo;
-          split16(pvv[e], h, lo);
-          ph[e] = h;
-          pl[e] = lo;
-        }
+      for (int e = 0; e < 8; ++e) {
+        _Float16 h, lo;
+        split16(sc[2 * t + (e >> 2)][e & 3], h, lo);
+        ph[e] = h;
+        pl[e] = lo;
       }
+      const _Float16* vr0 = vs + (32 * t + 4 * j + (n >> 2)) * kVS + 4 * (n & 3);
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const qlin::h8 vf = *reinterpret_cast<const qlin::h8*>(vt + (16 * c + n) * kVS + 32 * t + 8 * j);
-        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, vf, o[c], 0, 0, 0);
-        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl, vf, o[c], 0, 0, 0);
+        const uint2 lo4 = tr_read(vr0 + 16 * c);
+        const uint2 hi4 = tr_read(vr0 + 16 * kVS + 16 * c);
+        const qlin::h8 vf = __builtin_bit_cast(qlin::h8, make_uint4(lo4.x, lo4.y, hi4.x, hi4.y));
+        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, ph, o[c], 0, 0, 0);
+        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pl, o[c], 0, 0, 0);
       }
     }
   }
 
-  if (!wave_rows) return;
-  // O / (l 2^12) -> out[b][row][hq][d] (the layer's transpose(1, 2) layout; fp16 = its .to(fp16))
+  if (!wave_rows || row >= S) return;
+  // O / (l 2^12) -> out[b][row][hq][16 c + 4 j .. + 3] (the layer's transpose(1, 2) layout;
+  // fp16 = its .to(fp16))
+  const float rl = l * 4096.f;
+  const int64_t base = (((int64_t)b * S + row) * a.Hq + hq) * kD + 4 * j;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int row = row0 + 4 * j + e;
-    if (row >= S) continue;
-    const float rl = l[e] * 4096.f;
-    const int64_t base = (((int64_t)b * S + row) * a.Hq + hq) * kD + n;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const float val = o[c][e] / rl;
-      if (a.out_f16) reinterpret_cast<_Float16*>(a.out)[base + 16 * c] = (_Float16)val;
-      else reinterpret_cast<float*>(a.out)[base + 16 * c] = val;
+  for (int c = 0; c < 8; ++c) {
+    const f4v val = o[c] / rl;
+    if (a.out_f16) {
+      const qlin::h2 h01 = {(_Float16)val[0], (_Float16)val[1]};
+      const qlin::h2 h23 = {(_Float16)val[2], (_Float16)val[3]};
+      *reinterpret_cast<uint2*>(reinterpret_cast<_Float16*>(a.out) + base + 16 * c) =
+          make_uint2(qlin::as_u32(h01), qlin::as_u32(h23));
+    } else {
+      *reinterpret_cast<f4v*>(reinterpret_cast<float*>(a.out) + base + 16 * c) = val;
     }
   }
 }
@@ -311,7 +313,7 @@ extern "C" int qlin_attn_prefill(const float* q, const uint16_t* k, const uint16
   if (!q || !k || !v || !out || (out_dtype != QLIN_F32 && out_dtype != QLIN_F16) || B < 0 ||
       Hq <= 0 || Hkv <= 0 || Hq % Hkv || S <= 0 || L < S || L > (1 << 20) || D != kD ||
       !(scale_div > 0.f) || (mask && mask_dtype != QLIN_F16 && mask_dtype != QLIN_F32) ||
-      mask_batch_stride < 0 || (causal && !mask))
+      mask_batch_stride < 0 || causal < 0 || causal > 2 || (causal == 1 && !mask))
     return QLIN_EINVAL;
   const int G = Hq / Hkv;
   if (G > kMaxG || (G & (G - 1))) return QLIN_EINVAL;
@@ -325,7 +327,7 @@ extern "C" int qlin_attn_prefill(const float* q, const uint16_t* k, const uint16
   a.out = out;
   a.mask_f32 = mask_dtype == QLIN_F32;
   a.out_f16 = out_dtype == QLIN_F16;
-  a.causal = causal != 0;
+  a.causal = causal;
   a.Hq = Hq;
   a.Hkv = Hkv;
   a.S = (int)S;
@@ -337,7 +339,11 @@ extern "C" int qlin_attn_prefill(const float* q, const uint16_t* k, const uint16
   a.inv = 1.0f / scale_div;
   const int64_t blocks = B * Hkv * (G / a.hw) * (int64_t)a.nrb;
   if (blocks > 0x7fffffff) return QLIN_EINVAL;
-  hipLaunchKernelGGL(attn_prefill_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                     (hipStream_t)stream, a);
+  if (mask && causal != 2)
+    hipLaunchKernelGGL(attn_prefill_kernel<true>, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(attn_prefill_kernel<false>, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

@@ -518,10 +518,12 @@ def attn_prefill_supported(q, k, mask=None):
 _CAUSAL = {}
 
 
-def mask_is_causal(mask, S, L) -> bool:
-    """The additive mask [B', 1, S, L] leaves every key past a query's diagonal (key > L - S + i)
-    at <= -1e4 (so its exp() underflows to 0) and keeps the diagonal itself open; cached per
-    tensor version (one check per forward, the decoder layers share the mask)."""
+def mask_is_causal(mask, S, L) -> int:
+    """1 if the additive mask [B', 1, S, L] leaves every key past a query's diagonal
+    (key > L - S + i) at <= -1e4 (so its exp() underflows to 0) and keeps some key of every row
+    open, 2 if moreover every key on and below the diagonal is exactly 0 (the pure causal
+    pattern), else 0; cached per tensor version (one check per forward: the decoder layers share
+    the mask)."""
     key = (mask.data_ptr(), mask._version, tuple(mask.shape), tuple(mask.stride()), mask.dtype)
     hit = _CAUSAL.get(key)
     if hit is not None:
@@ -531,7 +533,9 @@ def mask_is_causal(mask, S, L) -> bool:
     above = j > (L - S) + i
     m = mask[:, 0].float()
     open_max = torch.where(above, torch.full_like(m, -float("inf")), m).amax(dim=-1)  # per row
-    ok = bool((m[:, above] <= -1e4).all()) and bool((open_max > -1e4).all())
+    ok = int(bool((m[:, above] <= -1e4).all()) and bool((open_max > -1e4).all()))
+    if ok and bool((m[:, ~above] == 0).all()):
+        ok = 2
     if len(_CAUSAL) > 64:
         _CAUSAL.clear()
     _CAUSAL[key] = ok

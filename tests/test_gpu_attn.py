@@ -138,7 +138,7 @@ def test_attn_prefill_matches_reference(B, Hq, Hkv, S, L, mask_kind):
     mask = None
     if mask_kind != "none":
         mask = _causal_mask(B, S, L, torch.float32 if mask_kind == "causal_f32" else torch.float16)
-        assert qlin.mask_is_causal(mask, S, L)
+        assert qlin.mask_is_causal(mask, S, L) == 2  # the pure pattern: applied, never read
     out = qlin.attn_prefill(q, k, v, mask, math.sqrt(128))
     ref = _ref(q, k, v, mask).transpose(1, 2)
     err = (out.double() - ref).abs().max().item()
@@ -156,7 +156,7 @@ def test_attn_prefill_padding_mask_is_not_causal():
     k = torch.randn(B, Hkv, S, 128, device="cuda", generator=g).half()
     v = torch.randn(B, Hkv, S, 128, device="cuda", generator=g).half()
     mask = _causal_mask(B, S, S, pad=[0, 70])
-    assert not qlin.mask_is_causal(mask, S, S)
+    assert qlin.mask_is_causal(mask, S, S) == 0
     out = qlin.attn_prefill(q, k, v, mask, math.sqrt(128))
     ref = _ref(q, k, v, mask).transpose(1, 2)
     # rows 0..69 of batch 1 see no open key: their scores are qk / sqrt(d) - 65504 quantised to
@@ -184,6 +184,7 @@ def test_attn_prefill_rejects_unsupported():
         qlin.attn_prefill(q, k, k, None, 8.0)
     lib = qlin.load_library()
     p = 16
-    # causal without a mask, odd group size
+    # mask-reading causal mode without a mask, bad mode, odd group size
     assert lib.qlin_attn_prefill(p, p, p, None, 0, 0, 1, p, 0, 1, 8, 8, 4, 4, 128, 11.3, None) == 1
+    assert lib.qlin_attn_prefill(p, p, p, p, 0, 0, 3, p, 0, 1, 8, 8, 4, 4, 128, 11.3, None) == 1
     assert lib.qlin_attn_prefill(p, p, p, None, 0, 0, 0, p, 0, 1, 24, 8, 4, 4, 128, 11.3, None) == 1
