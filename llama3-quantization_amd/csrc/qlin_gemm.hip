@@ -215,6 +215,90 @@ __device__ __forceinline__ void compute_stage(const unsigned char* st, const Gem
   step(std::integral_constant<int, 3>{});
 }
 
+// epilogue of a wave's MB x NB blocks of 16 x 16: lane (n, q) holds C[4q + i][n] of each block;
+// the wave's rows start at wrow0, its columns at 16-column tile ct0 (the block's rows at m0, BM
+// of them)
+template <int MB, int NB, int BM>
+__device__ __forceinline__ void store_tile(const f4 (&acc)[MB][NB], int64_t M, int N, int64_t m0,
+                                           int64_t wrow0, int64_t ct0, int lane,
+                                           const _Float16* __restrict__ bias,
+                                           _Float16* __restrict__ y,
+                                           const _Float16* __restrict__ res, int ep) {
+  const int n_in = lane & 15, q = lane >> 4;
+  if (ep == kEpSiluMul) {  // N % 16 == 0: gate column n_in < 8 pairs with up column n_in + 8
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int64_t j = ct0 + nb;  // interleaved tile = output columns 8j..8j+7
+      const int64_t n = j * kTileN + n_in;
+      const bool in_n = n < N;     // wave-uniform
+      const float bv = (bias && in_n) ? (float)bias[n] : 0.f;
+      // lane n_in < 8 holds gate column c = n_in, lane n_in + 8 the up column c, rows 4q + i:
+      // the pair splits the rows — the low lane forms rows 4q, 4q + 1, the high lane 4q + 2,
+      // 4q + 3 — so each SiLU is evaluated once (row_ror:8 swaps the halves of a 16-lane row)
+      const bool lo = n_in < 8;
+      const int c = n_in & 7;
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        float t[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] = (float)(_Float16)(acc[mb][nb][i] + bv);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          // what the partner lane needs: the low lane's gate of row 2 + h, the high lane's up
+          // of row h
+          const float r = dpp_f<0x128>(lo ? t[2 + h] : t[h]);
+          const float gv = lo ? t[h] : r, uv = lo ? r : t[2 + h];
+          const int64_t m = wrow0 + mb * 16 + 4 * q + (lo ? h : 2 + h);
+          if (in_n && m < M) y[m * (N >> 1) + j * 8 + c] = (_Float16)(silu_rn16(gv) * uv);
+        }
+      }
+    }
+    return;
+  }
+  if (m0 + BM <= M && (int64_t)BM * N < (1ll << 31)) {
+    // whole row tile inside M: a uniform row base and 32-bit per-lane offsets, no row checks
+    // (M = 65,536: 1151 -> 1206 TFLOP/s against the per-element checked stores below)
+    const int64_t base = wrow0 * (int64_t)N;
+    _Float16* __restrict__ yb = y + base;
+    const _Float16* __restrict__ rb = res + base;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int n = (int)((ct0 + nb) * kTileN) + n_in;
+      if (n >= N) continue;
+      const float bv = bias ? (float)bias[n] : 0.f;
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t o = (uint32_t)((mb * 16 + 4 * q + i) * N + n);
+          if (ep == kEpResidual)
+            yb[o] = (_Float16)((float)(_Float16)(acc[mb][nb][i] + bv) + (float)rb[o]);
+          else
+            yb[o] = (_Float16)(acc[mb][nb][i] + bv);
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int64_t n = (ct0 + nb) * kTileN + n_in;
+    if (n >= N) continue;
+    const float bv = bias ? (float)bias[n] : 0.f;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = wrow0 + mb * 16 + 4 * q + i;
+        if (m >= M) continue;
+        if (ep == kEpResidual)
+          y[m * N + n] = (_Float16)((float)(_Float16)(acc[mb][nb][i] + bv) + (float)res[m * N + n]);
+        else
+          y[m * N + n] = (_Float16)(acc[mb][nb][i] + bv);
+      }
+    }
+  }
+}
+
 // ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
 // the DMA after the first k-tile, bit 2 the dequant VALU; the library instantiates ABL = 0 only
 template <int BITS, int WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4>
@@ -263,81 +347,9 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
       compute_stage<BITS, WN_, GPT, ZM, KFULL, NW, ABL>(smem + (kt & 1) * C::STAGE, g, kt, acc);
   }
 
-  // epilogue: lane (n, q) holds C[4q + i][n] of each 16 x 16 block
   const int wm = g.wave / C::WGN, wn = g.wave % C::WGN;
-  const int n_in = g.lane & 15, q = g.lane >> 4;
-  if (ep == kEpSiluMul) {  // N % 16 == 0: gate column n_in < 8 pairs with up column n_in + 8
-#pragma unroll
-    for (int nb = 0; nb < C::NB; ++nb) {
-      const int64_t j = g.nt0 + wn * C::NB + nb;  // interleaved tile = output columns 8j..8j+7
-      const int64_t n = j * kTileN + n_in;
-      const bool in_n = n < N;                    // wave-uniform
-      const float bv = (bias && in_n) ? (float)bias[n] : 0.f;
-      // lane n_in < 8 holds gate column c = n_in, lane n_in + 8 the up column c, rows 4q + i:
-      // the pair splits the rows — the low lane forms rows 4q, 4q + 1, the high lane 4q + 2,
-      // 4q + 3 — so each SiLU is evaluated once (row_ror:8 swaps the halves of a 16-lane row)
-      const bool lo = n_in < 8;
-      const int c = n_in & 7;
-#pragma unroll
-      for (int mb = 0; mb < C::MB; ++mb) {
-        float t[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) t[i] = (float)(_Float16)(acc[mb][nb][i] + bv);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          // what the partner lane needs: the low lane's gate of row 2 + h, the high lane's up
-          // of row h
-          const float r = dpp_f<0x128>(lo ? t[2 + h] : t[h]);
-          const float gv = lo ? t[h] : r, uv = lo ? r : t[2 + h];
-          const int64_t m = g.m0 + wm * C::WM + mb * 16 + 4 * q + (lo ? h : 2 + h);
-          if (in_n && m < M) y[m * (N >> 1) + j * 8 + c] = (_Float16)(silu_rn16(gv) * uv);
-        }
-      }
-    }
-    return;
-  }
-  if (g.m0 + C::BM <= M && (int64_t)C::BM * N < (1ll << 31)) {
-    // whole row tile inside M: a uniform row base and 32-bit per-lane offsets, no row checks
-    // (M = 65,536: 1151 -> 1206 TFLOP/s against the per-element checked stores below)
-    const int64_t base = (g.m0 + wm * C::WM) * (int64_t)N;
-    _Float16* __restrict__ yb = y + base;
-    const _Float16* __restrict__ rb = res + base;
-#pragma unroll
-    for (int nb = 0; nb < C::NB; ++nb) {
-      const int n = (int)((g.nt0 + wn * C::NB + nb) * kTileN) + n_in;
-      if (n >= N) continue;
-      const float bv = bias ? (float)bias[n] : 0.f;
-#pragma unroll
-      for (int mb = 0; mb < C::MB; ++mb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t o = (uint32_t)((mb * 16 + 4 * q + i) * N + n);
-          if (ep == kEpResidual)
-            yb[o] = (_Float16)((float)(_Float16)(acc[mb][nb][i] + bv) + (float)rb[o]);
-          else
-            yb[o] = (_Float16)(acc[mb][nb][i] + bv);
-        }
-    }
-    return;
-  }
-#pragma unroll
-  for (int nb = 0; nb < C::NB; ++nb) {
-    const int64_t n = (g.nt0 + wn * C::NB + nb) * kTileN + n_in;
-    if (n >= N) continue;
-    const float bv = bias ? (float)bias[n] : 0.f;
-#pragma unroll
-    for (int mb = 0; mb < C::MB; ++mb) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t m = g.m0 + wm * C::WM + mb * 16 + 4 * q + i;
-        if (m >= M) continue;
-        if (ep == kEpResidual)
-          y[m * N + n] = (_Float16)((float)(_Float16)(acc[mb][nb][i] + bv) + (float)res[m * N + n]);
-        else
-          y[m * N + n] = (_Float16)(acc[mb][nb][i] + bv);
-      }
-    }
-  }
+  store_tile<C::MB, C::NB, C::BM>(acc, M, N, g.m0, g.m0 + wm * C::WM, g.nt0 + wn * C::NB, g.lane,
+                                  bias, y, res, ep);
 }
 
 uint32_t group_magic(int group) {
