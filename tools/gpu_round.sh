@@ -30,6 +30,6 @@ for s in $STEPS; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run \
          -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/pmc.log" 2>&1)
       rc=$?; echo "pmc rc=$rc"; tail -2 "$OUT/pmc.log"; ok_or_stop $rc pmc
-      python tools/pmc_traffic.py "$OUT/pmc" gemv_kernel "${PMC_WORKLOAD:-gemv_int4_g128}" "$OUT/pmc_traffic.json" ;;
+      python tools/pmc_traffic.py "$OUT/pmc" gemv_ "${PMC_WORKLOAD:-gemv_int4_g128}" "$OUT/pmc_traffic.json" ;;
   esac
 done

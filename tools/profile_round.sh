@@ -27,7 +27,7 @@ export TMPDIR=/tmp
 find "$OUT/kt" -name "*kernel_stats.csv" -exec cp {} "$OUT/${R}_gemv_int4_g128_kernel_stats.csv" \;
 (cd /tmp && step pmc 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run \
    -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $?
-python tools/pmc_traffic.py "$OUT/pmc" gemv_kernel gemv_int4_g128 "$OUT/${R}_gemv_int4_g128_pmc.json"
+python tools/pmc_traffic.py "$OUT/pmc" gemv_ gemv_int4_g128 "$OUT/${R}_gemv_int4_g128_pmc.json"
 step decode_layer 300 python tools/bench_decode.py
 step attn_prefill 300 python tools/dev/attn_prefill_bench.py
 step ppl_llama3_8b 500 python tools/ppl_llama3_8b.py
