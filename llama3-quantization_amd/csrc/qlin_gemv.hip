@@ -177,9 +177,14 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
       ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, ac, 0, 0, 0);
     }
   };
-  auto tile = [&](const WTile<BITS, GPT> (&t)[NTB], XRaw<MT>& xr, int kt, auto FULL_) {
+  // live == false: a slot past the wave's tiles (a repeat of its last tile), computed on x zeroed
+  auto tile = [&](const WTile<BITS, GPT> (&t)[NTB], XRaw<MT>& xr, int kt, auto FULL_, bool live) {
     h8 xa[4];
     if (aq.on) fake_quant_x<MT>(xr, aq, aq_sc, aq_zp);  // wave-uniform
+    if (!live) {  // wave-uniform
+#pragma unroll
+      for (int c = 0; c < MT; ++c) xr.w[c] = 0u;
+    }
     park_x<MT>(xa, xr, xslot, g.lane, g.n_in);
 #pragma unroll
     for (int j = 0; j < NTB; ++j) {
@@ -206,21 +211,22 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int kt = kt0 + t0 + u;
-      tile(wt[u], xq[u], kt, std::true_type{});
+      tile(wt[u], xq[u], kt, std::true_type{}, true);
       load_x<MT>(xq[u], g, min(kt + PF, ktl));
 #pragma unroll
       for (int j = 0; j < NTB; ++j) load_w<NTB>(wt[u][j], g, min(kt + PF, ktl), j);
     }
   }
   // last round (1..PF tiles): compute only; a tile short of K (the matrix's last) takes the
-  // per-k-step checks, every other one the straight-line body
+  // per-k-step checks, every other one the straight-line body.  Slots past the wave's tiles are
+  // computed too (their clamped repeat on x zeroed): under an `if (live)` the compiler sinks
+  // their loads into the branch, i.e. behind the earlier slots' dequant
 #pragma unroll
   for (int u = 0; u < PF; ++u) {
     const int kt = kt0 + t0 + u;
-    if (t0 + u < nts) {
-      if ((kt + 1) * kTileK <= g.K) tile(wt[u], xq[u], kt, std::true_type{});
-      else tile(wt[u], xq[u], kt, std::false_type{});
-    }
+    const bool live = t0 + u < nts;  // wave-uniform
+    if (!live || (kt + 1) * kTileK <= g.K) tile(wt[u], xq[u], kt, std::true_type{}, live);
+    else tile(wt[u], xq[u], kt, std::false_type{}, true);
   }
 
 }

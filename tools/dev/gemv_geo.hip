@@ -25,7 +25,7 @@ extern "C" int geo_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
 }
 
 // the decode fast path (gemv_fast_kernel) with an explicit geometry: W waves (power of two),
-// PF tiles in flight, LOOP = refill loop compiled in (required when ceil(Kt / W) > PF)
+// PF tiles in flight (every wave's tiles: ceil(Kt / W) <= PF); LOOP must be 0
 extern "C" int geo_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, uint16_t* y,
                         int N, int K, int W, int PF, int LOOP, void* stream) {
   const int Nt = (N + kTileN - 1) / kTileN;
@@ -36,11 +36,11 @@ extern "C" int geo_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t*
   while ((2 << lw) <= W) ++lw;
   a.W = 1 << lw; a.lw = lw; a.cmagic = 1u << 31;
   if ((a.Kt + a.W - 1) / a.W > PF && !LOOP) return 1;
-#define F(P, L) hipLaunchKernelGGL((gemv_fast_kernel<4, 1, 1, kZNarrow, kEpNone, P, L>), dim3(Nt), \
-                                   dim3(64 * a.W), 0, (hipStream_t)stream, a)
-  if (PF == 2) { if (LOOP) F(2, true); else F(2, false); }
-  else if (PF == 4) { if (LOOP) F(4, true); else F(4, false); }
-  else { if (LOOP) F(8, true); else F(8, false); }
+#define F(P) hipLaunchKernelGGL((gemv_fast_kernel<4, 1, 1, kZNarrow, kEpNone, P>), dim3(Nt), \
+                                dim3(64 * a.W), 0, (hipStream_t)stream, a)
+  if (LOOP) return 1;  // the product fast path has no refill loop (round 2)
+  if (PF == 2) F(2);
+  else F(4);
 #undef F
   return (int)hipGetLastError();
 }
