@@ -22,7 +22,7 @@ from quant import qlin
 from quant.int_linear import (FusedPackedLinear, QuantLinear, SiluMulPackedLinear, _same_act,
                               act_spec, packed_residual_linear)
 from quant.int_matmul import QuantMatMul
-from quant.omni_norm import OmniLlamaRMSNorm
+from quant.omni_norm import KERNEL_MAX_ROWS, OmniLlamaRMSNorm
 
 
 def _rope_theta(config):
@@ -394,6 +394,10 @@ class QuantLlamaDecoderLayer(nn.Module):
         self.fused_epilogues = self.self_attn.o_proj.packed and self.mlp.down_proj.packed
         self.input_layernorm.use_kernel = True
         self.post_attention_layernorm.use_kernel = True
+        # windows too take the RMSNorm kernel once the attention is no longer bit-exact anyway
+        rows = None if prefill_attention else KERNEL_MAX_ROWS
+        self.input_layernorm.kernel_max_rows = rows
+        self.post_attention_layernorm.kernel_max_rows = rows
         return self
 
     @torch.no_grad()

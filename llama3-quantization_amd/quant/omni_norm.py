@@ -3,7 +3,9 @@
 RMSNorm is computed in fp32 and cast back, exactly as the reference does, with torch ops on the
 device; in the fused packed decoder layer (``use_kernel``, set by
 ``QuantLlamaDecoderLayer.fuse_packed_projections``) decode-sized inputs (<= 64 rows) take one
-gfx950 launch (``qlin_rmsnorm_f16``, same arithmetic, sum of squares in another order).
+gfx950 launch (``qlin_rmsnorm_f16``, same arithmetic, sum of squares in another order); with the
+prefill-attention kernel (already equal to the reference to fp32 rounding, not bit for bit) every
+input does (``kernel_max_rows = None``).
 """
 import torch
 import torch.nn as nn
@@ -50,6 +52,7 @@ class OmniLlamaRMSNorm(nn.Module):
         self.variance_epsilon = eps
         self.use_temporary_parameter = False
         self.use_kernel = False
+        self.kernel_max_rows = KERNEL_MAX_ROWS  # None: every input takes the kernel
         self._w32 = None
 
     def _kernel_weight(self):
@@ -61,7 +64,8 @@ class OmniLlamaRMSNorm(nn.Module):
     def forward(self, hidden_states):
         if (self.use_kernel and not self.use_temporary_parameter and self.bias is None
                 and hidden_states.is_cuda and hidden_states.dtype == torch.float16
-                and hidden_states.numel() <= KERNEL_MAX_ROWS * hidden_states.shape[-1]):
+                and (self.kernel_max_rows is None
+                     or hidden_states.numel() <= self.kernel_max_rows * hidden_states.shape[-1])):
             return qlin.rmsnorm(hidden_states.contiguous(), self._kernel_weight(),
                                 self.variance_epsilon)
         input_dtype = hidden_states.dtype
