@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 3
+#define QLIN_ABI_VERSION 4
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -183,7 +183,9 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
  * attention core (models/int_llama_layer.py:137-165 of the reference: repeat_kv, fp32 QK^T bmm,
  * / sqrt(head_dim), + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV bmm) on an fp16 K/V
  * cache; fp32 arithmetic, equal to the reference up to fp32 summation order.
- *   q    fp32 [B, Hq, D] (after RoPE);  k, v  fp16 [B, Hkv, L, D];  mask  fp16 [B, L] additive or
+ *   q    fp32 [B, Hq, D] (after RoPE);  k, v  fp16 [B, Hkv, L, D], the L rows of (b, kv head h)
+ *   at k + (b * Hkv + h) * kv_head_stride elements (0: L * D, contiguous; else a multiple of 8,
+ *   >= L * D: a KV cache with spare rows, see qlin_rope_kv_f16);  mask  fp16 [B, L] additive or
  *   NULL;  out  [B, Hq, D] in out_dtype: QLIN_F32, or QLIN_F16 = the fp32 result rounded once
  *   (the layer's .to(fp16) before o_proj);  scale_div = sqrt(D) (the scores are divided by it).
  *   D == 128, Hq / Hkv in {1, 2, 4, 8}, L <= 4096.
@@ -196,7 +198,8 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
 int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L);
 int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
                      void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int D,
-                     float scale_div, float* partials, int32_t* counters, void* stream);
+                     int64_t kv_head_stride, float scale_div, float* partials, int32_t* counters,
+                     void* stream);
 
 /*
  * Fused prefill attention (many query tokens per sequence): the same attention core as
@@ -247,6 +250,22 @@ int qlin_rope_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k, in
                   const float* cos_cache, const float* sin_cache, int64_t cache_rows,
                   const int64_t* position_ids, int64_t pos_batch_stride, float* q_out, uint16_t* k_out, int64_t B, int64_t S,
                   int Hq, int Hkv, int D, void* stream);
+
+/*
+ * qlin_rope_f16 plus the KV-cache append of the same layer step (models/int_llama_layer.py:130-135
+ * of the reference: torch.cat([past_key, key], dim=2), likewise for value): the rotated k rows and
+ * the v rows (v  fp16 rows of Hkv*D at v + (b*S + s)*v_row_stride) are written straight into
+ * caches k_cache / v_cache fp16 [B, Hkv, kv_rows, D] at rows kv0 .. kv0 + S - 1, so the cached
+ * rows 0 .. kv0 - 1 are never copied.  Requires D % 8 == 0, q / k / v strides and pointers
+ * 4-element aligned, cos / sin / q_out 16-B aligned and kv0 + S <= kv_rows (else
+ * QLIN_EINVAL).  Same arithmetic as qlin_rope_f16 (bit-exact).
+ */
+int qlin_rope_kv_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+                     int64_t k_row_stride, const uint16_t* v, int64_t v_row_stride,
+                     const float* cos_cache, const float* sin_cache, int64_t cache_rows,
+                     const int64_t* position_ids, int64_t pos_batch_stride, float* q_out,
+                     uint16_t* k_cache, uint16_t* v_cache, int64_t kv_rows, int64_t kv0,
+                     int64_t B, int64_t S, int Hq, int Hkv, int D, void* stream);
 
 /*
  * Attention scores of a prefill window, in place (models/int_llama_layer.py:143-157 of the

@@ -90,7 +90,7 @@ template <int GRP>
 __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
     const float* __restrict__ q, const _Float16* __restrict__ k, const _Float16* __restrict__ v,
     const _Float16* __restrict__ mask, void* __restrict__ out, int out_f16, int Hq, int Hkv,
-    int L, int chunk,
+    int L, int64_t kv_hs, int chunk,
     int S, float scale_div, int* __restrict__ counters, float* __restrict__ part_o,
     float* __restrict__ part_ml) {
   __shared__ float qs[GRP][kD];
@@ -109,8 +109,10 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   const int t0 = split * chunk;
   const int n = min(chunk, L - t0);  // positions in this chunk (>= 1)
 
-  const _Float16* kb = k + ((int64_t)bh * L + t0) * kD;
-  const uint32_t* vb = reinterpret_cast<const uint32_t*>(v + ((int64_t)bh * L + t0) * kD) + lane;
+  // cache rows of (b, kv head) bh start at bh * kv_hs (a KV cache with spare rows: kv_hs > L * kD)
+  const _Float16* kb = k + (int64_t)bh * kv_hs + (int64_t)t0 * kD;
+  const uint32_t* vb =
+      reinterpret_cast<const uint32_t*>(v + (int64_t)bh * kv_hs + (int64_t)t0 * kD) + lane;
   const _Float16* mb = mask ? mask + (int64_t)b * L + t0 : nullptr;
 
   // issue the first pass's K rows, V words and mask before anything waits
@@ -334,12 +336,14 @@ extern "C" int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, i
 extern "C" int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v,
                                 const uint16_t* mask, void* out, int out_dtype, int64_t B,
                                 int Hq, int Hkv,
-                                int64_t L, int D, float scale_div, float* partials,
-                                int32_t* counters, void* stream) {
+                                int64_t L, int D, int64_t kv_head_stride, float scale_div,
+                                float* partials, int32_t* counters, void* stream) {
   if (!q || !k || !v || !out || (out_dtype != QLIN_F32 && out_dtype != QLIN_F16) || B < 0 ||
       Hq <= 0 || Hkv <= 0 || Hq % Hkv || L <= 0 ||
-      L > kMaxL || D != kD || B * Hkv > 0x7fffffff)
+      L > kMaxL || D != kD || B * Hkv > 0x7fffffff ||
+      (kv_head_stride != 0 && (kv_head_stride < L * kD || kv_head_stride % 8)))
     return QLIN_EINVAL;
+  const int64_t kv_hs = kv_head_stride ? kv_head_stride : L * kD;
   const int grp = Hq / Hkv;
   if (grp > kMaxGroup) return QLIN_EINVAL;
   if (B == 0) return QLIN_OK;
@@ -358,7 +362,7 @@ extern "C" int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_
   hipLaunchKernelGGL((attn_decode_kernel<G>), grid, dim3(kThreads), 0, st, q,                 \
                      (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,        \
                      out_dtype == QLIN_F16, Hq,                                                 \
-                     Hkv, (int)L, sp.chunk, sp.S, scale_div, (int*)counters, part_o, part_ml)
+                     Hkv, (int)L, kv_hs, sp.chunk, sp.S, scale_div, (int*)counters, part_o, part_ml)
   switch (grp) {
     case 1: QLIN_A(1); break;
     case 2: QLIN_A(2); break;

@@ -12,7 +12,12 @@
 // the q/k reshape + transpose, q's cast to fp32, rotary_emb(cos/sin cache slice, cast to fp16)
 // and apply_rotary_pos_emb (index by position_ids, q*cos + rotate_half(q)*sin in fp32 for q,
 // the same in fp16 for k: every product and the sum rounded to fp16 as torch's fp16 ops do).
-// Elementwise with the reference's op order and roundings: bit-exact.
+// Elementwise with the reference's op order and roundings: bit-exact.  One block per token row
+// (the position and the cos / sin rows read once per block), each thread rotating four
+// (d, d + D/2) pairs with 8-B / 16-B accesses; qlin_rope_kv_f16 also writes the rotated k and
+// the v row straight into a KV cache at row kv0 + s (the reference's torch.cat of the cache,
+// models/int_llama_layer.py:130-135, without re-copying the cache).  A 2048-token window:
+// 50 us (one thread per element, 64-bit index math) -> see DESIGN.md §4.
 //
 // qlin_attn_scores_f32 replaces, for prefill windows, the three fp32 passes over the
 // [B, H, T, L] score tensor after QK^T (models/int_llama_layer.py:143-157: / sqrt(head_dim),
@@ -137,6 +142,111 @@ __global__ __launch_bounds__(256) void rope_kernel(
   }
 }
 
+struct RopeArgs {
+  const _Float16* q;
+  int64_t q_rs;
+  const _Float16* k;
+  int64_t k_rs;
+  const _Float16* v;  // nullptr: no v copy
+  int64_t v_rs;
+  const float* cosc;
+  const float* sinc;
+  int64_t cache_rows;
+  const int64_t* pos;
+  int64_t pos_bs;
+  float* q_out;      // [B, Hq, S, D]
+  _Float16* k_out;   // [B, Hkv, kv_rows, D], rows kv0 .. kv0 + S - 1 written
+  _Float16* v_out;
+  int64_t kv_rows, kv0;
+  int S, Hq, Hkv, D;
+};
+
+// one block per (b, s); D % 8 == 0, q / k / v rows and strides 4-element aligned, outputs 16-B
+// aligned (checked on the host)
+__global__ __launch_bounds__(256) void rope_rows_kernel(RopeArgs a) {
+#pragma clang fp contract(off)
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const int64_t bs = blockIdx.x;
+  const int64_t b = bs / a.S;
+  const int s = (int)(bs - b * a.S);
+  const int64_t p = min(max(a.pos[b * a.pos_bs + s], (int64_t)0), a.cache_rows - 1);
+  const int D = a.D, half = D >> 1, nq = half >> 2;
+  const float* cr = a.cosc + p * D;
+  const float* sr = a.sinc + p * D;
+  const int items = (a.Hq + a.Hkv) * nq;
+  for (int it = threadIdx.x; it < items; it += 256) {
+    const int h = it / nq, d0 = (it - h * nq) * 4;
+    const float4 cl4 = *reinterpret_cast<const float4*>(cr + d0);
+    const float4 ch4 = *reinterpret_cast<const float4*>(cr + d0 + half);
+    const float4 sl4 = *reinterpret_cast<const float4*>(sr + d0);
+    const float4 sh4 = *reinterpret_cast<const float4*>(sr + d0 + half);
+    // the reference's cos / sin: the fp32 cache cast to the activation dtype (fp16)
+    const float cl[4] = {(float)(_Float16)cl4.x, (float)(_Float16)cl4.y, (float)(_Float16)cl4.z,
+                         (float)(_Float16)cl4.w};
+    const float chh[4] = {(float)(_Float16)ch4.x, (float)(_Float16)ch4.y, (float)(_Float16)ch4.z,
+                          (float)(_Float16)ch4.w};
+    const float sl[4] = {(float)(_Float16)sl4.x, (float)(_Float16)sl4.y, (float)(_Float16)sl4.z,
+                         (float)(_Float16)sl4.w};
+    const float shh[4] = {(float)(_Float16)sh4.x, (float)(_Float16)sh4.y, (float)(_Float16)sh4.z,
+                          (float)(_Float16)sh4.w};
+    if (h < a.Hq) {
+      const _Float16* qr = a.q + (b * a.S + s) * a.q_rs + (int64_t)h * D;
+      const h4 lo = *reinterpret_cast<const h4*>(qr + d0);
+      const h4 hi = *reinterpret_cast<const h4*>(qr + d0 + half);
+      float ol[4], oh[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // fp32: q * cos + rotate_half(q) * sin, rotate_half = (-q[d + D/2], q[d - D/2])
+        ol[j] = (float)lo[j] * cl[j] + (-(float)hi[j]) * sl[j];
+        oh[j] = (float)hi[j] * chh[j] + (float)lo[j] * shh[j];
+      }
+      float* qo = a.q_out + ((b * a.Hq + h) * a.S + s) * (int64_t)D;
+      *reinterpret_cast<float4*>(qo + d0) = make_float4(ol[0], ol[1], ol[2], ol[3]);
+      *reinterpret_cast<float4*>(qo + d0 + half) = make_float4(oh[0], oh[1], oh[2], oh[3]);
+    } else {
+      const int hk = h - a.Hq;
+      const _Float16* kr = a.k + (b * a.S + s) * a.k_rs + (int64_t)hk * D;
+      const h4 lo = *reinterpret_cast<const h4*>(kr + d0);
+      const h4 hi = *reinterpret_cast<const h4*>(kr + d0 + half);
+      h4 ol, oh;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // fp16 ops: every product and the sum rounded to fp16
+        const float a0 = (float)(_Float16)((float)lo[j] * cl[j]);
+        const float b0 = (float)(_Float16)((-(float)hi[j]) * sl[j]);
+        ol[j] = (_Float16)(a0 + b0);
+        const float a1 = (float)(_Float16)((float)hi[j] * chh[j]);
+        const float b1 = (float)(_Float16)((float)lo[j] * shh[j]);
+        oh[j] = (_Float16)(a1 + b1);
+      }
+      _Float16* ko = a.k_out + ((b * a.Hkv + hk) * a.kv_rows + a.kv0 + s) * (int64_t)D;
+      *reinterpret_cast<h4*>(ko + d0) = ol;
+      *reinterpret_cast<h4*>(ko + d0 + half) = oh;
+    }
+  }
+  if (a.v) {  // the v row into the cache (8 halves per thread and step)
+    const int nv = a.Hkv * (D >> 3);
+    for (int it = threadIdx.x; it < nv; it += 256) {
+      const int hk = it / (D >> 3), d0 = (it - hk * (D >> 3)) * 8;
+      const _Float16* vr = a.v + (b * a.S + s) * a.v_rs + (int64_t)hk * D + d0;
+      typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+      const h4v v0 = *reinterpret_cast<const h4v*>(vr);
+      const h4v v1 = *reinterpret_cast<const h4v*>(vr + 4);
+      _Float16* vo = a.v_out + ((b * a.Hkv + hk) * a.kv_rows + a.kv0 + s) * (int64_t)D + d0;
+      *reinterpret_cast<h4v*>(vo) = v0;
+      *reinterpret_cast<h4v*>(vo + 4) = v1;
+    }
+  }
+}
+
+// the vector kernel's alignment / shape conditions
+bool rope_rows_ok(const RopeArgs& a) {
+  const auto al = [](const void* p, uintptr_t n) { return ((uintptr_t)p % n) == 0; };
+  return a.D % 8 == 0 && a.q_rs % 4 == 0 && a.k_rs % 4 == 0 && al(a.q, 8) && al(a.k, 8) &&
+         al(a.cosc, 16) && al(a.sinc, 16) && al(a.q_out, 16) && al(a.k_out, 8) &&
+         (!a.v || (a.v_rs % 4 == 0 && al(a.v, 8) && al(a.v_out, 8)));
+}
+
 // attention scores of a prefill window, in place: w = max(w / scale + mask, finfo(fp32).min)
 // (w / scale alone without a mask)
 // with torch's scalar division (multiplication by the fp32 reciprocal), one pass instead of three
@@ -228,9 +338,41 @@ extern "C" int qlin_rope_f16(const uint16_t* q, int64_t q_row_stride, const uint
   const int64_t total = B * S * (int64_t)(Hq + Hkv) * D;
   if (total == 0) return QLIN_OK;
   if ((total + 255) / 256 > 0x7fffffff) return QLIN_EINVAL;
+  const RopeArgs ra{(const _Float16*)q, q_row_stride, (const _Float16*)k, k_row_stride, nullptr, 0,
+                    cos_cache, sin_cache, cache_rows, position_ids, pos_batch_stride, q_out,
+                    (_Float16*)k_out, nullptr, S, 0, (int)S, Hq, Hkv, D};
+  if (rope_rows_ok(ra) && B * S <= 0x7fffffff && S <= 0x7fffffff) {
+    hipLaunchKernelGGL(rope_rows_kernel, dim3((unsigned)(B * S)), dim3(256), 0,
+                       (hipStream_t)stream, ra);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(rope_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, (const _Float16*)q, q_row_stride, (const _Float16*)k,
                      k_row_stride, cos_cache, sin_cache, cache_rows, position_ids,
                      pos_batch_stride, q_out, (_Float16*)k_out, B, S, Hq, Hkv, D);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qlin_rope_kv_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+                                int64_t k_row_stride, const uint16_t* v, int64_t v_row_stride,
+                                const float* cos_cache, const float* sin_cache, int64_t cache_rows,
+                                const int64_t* position_ids, int64_t pos_batch_stride,
+                                float* q_out, uint16_t* k_cache, uint16_t* v_cache,
+                                int64_t kv_rows, int64_t kv0, int64_t B, int64_t S, int Hq,
+                                int Hkv, int D, void* stream) {
+  if (!q || !k || !v || !cos_cache || !sin_cache || !position_ids || !q_out || !k_cache ||
+      !v_cache || B < 0 || S < 0 || Hq <= 0 || Hkv <= 0 || D <= 0 ||
+      q_row_stride < (int64_t)Hq * D || k_row_stride < (int64_t)Hkv * D ||
+      v_row_stride < (int64_t)Hkv * D || pos_batch_stride < 0 || cache_rows <= 0 || kv0 < 0 ||
+      kv0 + S > kv_rows || B * S > 0x7fffffff || S > 0x7fffffff)
+    return QLIN_EINVAL;
+  const RopeArgs ra{(const _Float16*)q, q_row_stride, (const _Float16*)k, k_row_stride,
+                    (const _Float16*)v, v_row_stride, cos_cache, sin_cache, cache_rows,
+                    position_ids, pos_batch_stride, q_out, (_Float16*)k_cache,
+                    (_Float16*)v_cache, kv_rows, kv0, (int)S, Hq, Hkv, D};
+  if (!rope_rows_ok(ra)) return QLIN_EINVAL;
+  if (B * S == 0) return QLIN_OK;
+  hipLaunchKernelGGL(rope_rows_kernel, dim3((unsigned)(B * S)), dim3(256), 0, (hipStream_t)stream,
+                     ra);
   return (int)hipGetLastError();
 }

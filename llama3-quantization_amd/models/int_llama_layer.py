@@ -168,17 +168,66 @@ class QuantLlamaAttention(nn.Module):
         self.decode_kernel = False  # qlin_attn_decode for one-token steps (fuse_packed turns it on)
         self.rope_kernel = False  # qlin_rope_f16 (fuse_packed turns it on)
         self.prefill_kernel = False  # qlin_attn_prefill for multi-token windows (opt-in)
+        self.kv_cache = False  # rope + KV append into a preallocated cache (opt-in)
+        self._kv = None  # (k, v) cache buffers [B, Hkv, rows, D] of the kv_cache mode
 
-    def fuse_packed(self, prefill_attention: bool = False):
+    def fuse_packed(self, prefill_attention: bool = False, kv_cache: bool = False):
         """q_proj + k_proj + v_proj as one fused packed launch (all read the normed hidden), and
         the fused decode-attention kernel for one-token steps; ``prefill_attention`` also routes
         multi-token windows through the fused prefill-attention kernel (fp32, online softmax:
-        equal to the reference attention to fp32 rounding instead of bit for bit)."""
+        equal to the reference attention to fp32 rounding instead of bit for bit).
+
+        ``kv_cache``: with ``use_cache`` / a ``past_key_value``, RoPE writes the step's k and v
+        rows straight into cache buffers owned by the module and the returned ``past_key_value``
+        are row-prefix views of them, so a decode step appends two rows instead of re-copying the
+        whole cache (the reference's ``torch.cat``, models/int_llama_layer.py:130-135; the values
+        are identical).  A ``past_key_value`` that is not such a view (the first step, a reordered
+        beam) is copied into a fresh buffer once.  Two continuations of the SAME past share its
+        buffer and overwrite each other's next row, so this is opt-in."""
         self.qkv = FusedPackedLinear([self.q_proj, self.k_proj, self.v_proj])
         self.decode_kernel = True
         self.rope_kernel = hasattr(self.rotary_emb, "cos_cached")
         self.prefill_kernel = bool(prefill_attention)
+        self.kv_cache = bool(kv_cache)
         return self
+
+    def adopt_kv_cache(self, past_key_value, rows=None, batch=1, device=None):
+        """kv_cache mode: copy ``past_key_value`` (fp16 [B, Hkv, L, D] each, or None) into fresh
+        cache buffers with room to grow (2x the rows needed, at least 256) and return it as views
+        of them, which later steps append to in place."""
+        H, D = self.num_key_value_heads, self.head_dim
+        L0 = past_key_value[0].shape[-2] if past_key_value is not None else 0
+        if past_key_value is not None:
+            batch, device = past_key_value[0].shape[0], past_key_value[0].device
+        need = max(L0, rows or 0)
+        cap = max(256, (2 * need + 255) // 256 * 256)
+        kb = torch.empty(batch, H, cap, D, dtype=torch.float16, device=device)
+        vb = torch.empty_like(kb)
+        if past_key_value is not None:
+            kb[:, :, :L0].copy_(past_key_value[0])
+            vb[:, :, :L0].copy_(past_key_value[1])
+        self._kv = (kb, vb)
+        return (kb[:, :, :L0], vb[:, :, :L0])
+
+    def _rope_append(self, q, k, v, cos_c, sin_c, position_ids, past, bsz, q_len):
+        """kv_cache mode: RoPE + the cache append in one launch (qlin_rope_kv_f16); returns
+        (query_states, key_states, value_states) with k / v as views of the cache buffers."""
+        H, D = self.num_key_value_heads, self.head_dim
+        L0 = past[0].shape[-2] if past is not None else 0
+        need = L0 + q_len
+        buf = self._kv
+        inplace = (past is not None and buf is not None and need <= buf[0].shape[2]
+                   and past[0].data_ptr() == buf[0].data_ptr()
+                   and past[1].data_ptr() == buf[1].data_ptr()
+                   and tuple(past[0].shape) == (bsz, H, L0, D)
+                   and tuple(past[1].shape) == (bsz, H, L0, D)
+                   and past[0].stride() == buf[0].stride() and past[1].stride() == buf[1].stride())
+        if not inplace:
+            self.adopt_kv_cache(past, rows=need, batch=bsz, device=q.device)
+            buf = self._kv
+        query_states = qlin.rope_kv(q, k, v, cos_c, sin_c, position_ids, self.num_heads, H, D,
+                                    buf[0], buf[1], L0)
+        return query_states, buf[0][:, :, :need], buf[1][:, :, :need]
 
     def _attn_bypassed(self):
         """QuantMatMul quantizers are identity (abits >= 16 or act quant off)."""
@@ -238,18 +287,27 @@ class QuantLlamaAttention(nn.Module):
             kv_seq_len += past_key_value[0].shape[-2]
         if position_ids is None:
             position_ids = torch.arange(kv_seq_len - q_len, kv_seq_len, device=hidden_states.device)[None]
+        appended = False
         if self.rope_kernel and q.dtype == torch.float16 and q.is_cuda:
             # one launch: reshape/transpose, q -> fp32, cos/sin slice + cast, apply_rotary_pos_emb
             cos_c, sin_c = self._rope_cache(value_states, kv_seq_len)
-            query_states, key_states = qlin.rope(q, k, cos_c, sin_c, position_ids, self.num_heads,
-                                                 self.num_key_value_heads, self.head_dim)
+            if self.kv_cache and (use_cache or past_key_value is not None) and \
+                    (past_key_value is None or past_key_value[0].dtype == torch.float16):
+                # ... plus the cache append (kv_cache mode)
+                query_states, key_states, value_states = self._rope_append(
+                    q, k, v, cos_c, sin_c, position_ids, past_key_value, bsz, q_len)
+                appended = True
+            else:
+                query_states, key_states = qlin.rope(q, k, cos_c, sin_c, position_ids,
+                                                     self.num_heads, self.num_key_value_heads,
+                                                     self.head_dim)
         else:
             query_states = q.reshape(bsz, q_len, self.num_heads, self.head_dim).transpose(1, 2).type(torch.float32)
             key_states = k.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
             cos, sin = self.rotary_emb(value_states, seq_len=kv_seq_len)
             query_states, key_states = apply_rotary_pos_emb(query_states, key_states, cos, sin, position_ids)
 
-        if past_key_value is not None:
+        if past_key_value is not None and not appended:
             key_states = torch.cat([past_key_value[0], key_states], dim=2)
             value_states = torch.cat([past_key_value[1], value_states], dim=2)
         past_key_value = (key_states, value_states) if use_cache else None
@@ -385,11 +443,12 @@ class QuantLlamaDecoderLayer(nn.Module):
             if isinstance(m, (QuantLinear, QuantMatMul)):
                 m.set_quant_state(weight_quant, act_quant)
 
-    def fuse_packed_projections(self, prefill_attention: bool = False):
+    def fuse_packed_projections(self, prefill_attention: bool = False, kv_cache: bool = False):
         """After packing: q/k/v and gate/up (+ SiLU·mul) each become one fused launch, and the two
         residual adds move into the o_proj / down_proj epilogues (SURVEY.md §8 f4);
-        ``prefill_attention``: multi-token windows also take the fused prefill-attention kernel."""
-        self.self_attn.fuse_packed(prefill_attention)
+        ``prefill_attention``: multi-token windows also take the fused prefill-attention kernel;
+        ``kv_cache``: decode steps append to a preallocated KV cache (QuantLlamaAttention.fuse_packed)."""
+        self.self_attn.fuse_packed(prefill_attention, kv_cache)
         self.mlp.fuse_packed()
         self.fused_epilogues = self.self_attn.o_proj.packed and self.mlp.down_proj.packed
         self.input_layernorm.use_kernel = True

@@ -16,7 +16,7 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -51,11 +51,14 @@ SIGNATURES = {
                            _i),
     "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),
     "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
+    "qlin_rope_kv_f16": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _p, _l, _l, _l, _l,
+                          _i, _i, _i, _p], _i),
     "qlin_attn_scores_f32": ([_p, _p, _i, _l, _l, _l, _l, _l, ctypes.c_float, _p], _i),
     "qlin_attn_decode_partials_bytes": ([_l, _i, _i, _l], _l),
     "qlin_attn_prefill": ([_p, _p, _p, _p, _i, _l, _i, _p, _i, _l, _i, _i, _l, _l, _i,
                            ctypes.c_float, _p], _i),
-    "qlin_attn_decode": ([_p, _p, _p, _p, _p, _i, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p],
+    "qlin_attn_decode": ([_p, _p, _p, _p, _p, _i, _l, _i, _i, _l, _i, _l, ctypes.c_float, _p, _p,
+                          _p],
                          _i),
 }
 
@@ -104,6 +107,13 @@ def _dev(*ts):
                                "(no CPU fallback exists)")
         if not t.is_contiguous():
             raise ValueError("qlin kernels need contiguous tensors")
+
+
+def _on_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("qlin kernels run on gfx950 only: got a CPU tensor "
+                               "(no CPU fallback exists)")
 
 
 def _ptr(t):
@@ -419,6 +429,51 @@ def rope(q, k, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim
     return q_out, k_out
 
 
+def _pos_ids(position_ids, B, S):
+    pos = position_ids
+    if pos.dtype != torch.int64:
+        pos = pos.to(torch.int64)
+    if pos.dim() == 1:
+        pos = pos[None]
+    if pos.stride(-1) != 1:
+        pos = pos.contiguous()
+    if pos.shape[-1] != S or pos.shape[0] not in (1, B):
+        raise ValueError(f"position_ids {tuple(pos.shape)} do not match [B={B}, S={S}]")
+    return pos, (pos.stride(0) if pos.shape[0] > 1 else 0)
+
+
+def rope_kv(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim,
+            k_cache, v_cache, kv0):
+    """``qlin_rope_kv_f16``: ``rope`` plus the KV-cache append of the step. q [B, S, Hq*D],
+    k / v [B, S, Hkv*D] fp16 row-strided views; k_cache / v_cache fp16 [B, Hkv, rows, D]
+    contiguous buffers, rows kv0 .. kv0 + S - 1 written in place (the rotated k, and v).
+    Returns q_rot fp32 [B, Hq, S, D] (the reference's apply_rotary_pos_emb output for q)."""
+    for t_ in (q, k, v):
+        if _rows(t_) is None:
+            raise ValueError("rope_kv takes row-strided [B, S, H*D] q / k / v")
+    for t_ in (q, k, v, cos_cache, sin_cache, position_ids, k_cache, v_cache):
+        if not t_.is_cuda:
+            raise RuntimeError("qlin kernels run on gfx950 only: got a CPU tensor")
+    if q.dtype != torch.float16 or k.dtype != torch.float16 or v.dtype != torch.float16 or \
+            k_cache.dtype != torch.float16 or v_cache.dtype != torch.float16:
+        raise ValueError("rope_kv takes fp16 q / k / v and caches")
+    if not (k_cache.is_contiguous() and v_cache.is_contiguous()) or k_cache.shape != v_cache.shape:
+        raise ValueError("rope_kv takes contiguous [B, Hkv, rows, D] caches of one shape")
+    B, S = q.shape[0], q.shape[1]
+    if tuple(k_cache.shape[:2]) != (B, n_kv_heads) or k_cache.shape[3] != head_dim:
+        raise ValueError(f"cache {tuple(k_cache.shape)} does not match [B={B}, Hkv={n_kv_heads}, ., D]")
+    if kv0 < 0 or kv0 + S > k_cache.shape[2]:
+        raise ValueError(f"cache rows {k_cache.shape[2]} cannot take rows {kv0} .. {kv0 + S - 1}")
+    pos, pbs = _pos_ids(position_ids, B, S)
+    q_out = torch.empty(B, n_heads, S, head_dim, dtype=torch.float32, device=q.device)
+    rc = load_library().qlin_rope_kv_f16(
+        _ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(v), _rows(v), _ptr(cos_cache),
+        _ptr(sin_cache), cos_cache.shape[0], _ptr(pos), pbs, _ptr(q_out), _ptr(k_cache),
+        _ptr(v_cache), k_cache.shape[2], kv0, B, S, n_heads, n_kv_heads, head_dim, _stream(q))
+    _check(rc, "qlin_rope_kv_f16")
+    return q_out
+
+
 def attn_scores_(w, mask, scale_div):
     """In place: w = max(w / scale_div + mask, finfo(fp32).min) (``qlin_attn_scores_f32``); w fp32
     [B, H, T, L] contiguous, mask [B or 1, 1, T, L] fp16/fp32 or None.  Returns w."""
@@ -471,17 +526,32 @@ def _attn_counters(device, heads):
     return c
 
 
+def _cache_head_stride(k, v):
+    """Head stride (elements) when k / v [B, Hkv, L, D] are row-prefix views of contiguous
+    [B, Hkv, rows, D] cache buffers (rope_kv), else None (the caller makes them contiguous)."""
+    if k.stride() != v.stride() or k.stride(3) != 1 or k.stride(2) != k.shape[3]:
+        return None
+    hs = k.stride(1)
+    if hs < k.shape[2] * k.shape[3] or hs % 8 or (k.shape[0] > 1 and k.stride(0) != k.shape[1] * hs):
+        return None
+    return hs
+
+
 def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32):
     """softmax(q k^T / scale_div + mask) v for one query token: q fp32 [B, Hq, 1, D], k/v fp16
     [B, Hkv, L, D], mask fp16 [B, 1, 1, L] or None -> [B, Hq, 1, D] in out_dtype (fp32, or the
-    fp32 result rounded to fp16 in the kernel)."""
-    _dev(q, k, v)
+    fp32 result rounded to fp16 in the kernel); k / v may be row-prefix views of KV cache
+    buffers (rope_kv), read in place."""
+    _on_gpu(q, k, v)
     if not attn_decode_supported(q, k, mask):
         raise ValueError("attn_decode: unsupported shapes / dtypes")
     B, Hq, _, D = q.shape
     Hkv, L = k.shape[1], k.shape[2]
-    k = k.contiguous()
-    v = v.contiguous()
+    hs = _cache_head_stride(k, v)
+    if hs is None:
+        k = k.contiguous()
+        v = v.contiguous()
+        hs = 0
     m = None
     if mask is not None:
         m = mask.reshape(B, L).contiguous() if mask.shape[0] == B else \
@@ -497,7 +567,7 @@ def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32):
         cnt = _attn_counters(q.device, B * Hkv)
     rc = lib.qlin_attn_decode(_ptr(q.contiguous()), _ptr(k), _ptr(v), _ptr(m), _ptr(out),
                               _dtcode(out),
-                              B, Hq, Hkv, L, D, float(scale_div), _ptr(part), _ptr(cnt),
+                              B, Hq, Hkv, L, D, hs, float(scale_div), _ptr(part), _ptr(cnt),
                               _stream(q))
     _check(rc, "qlin_attn_decode")
     return out

@@ -71,6 +71,22 @@ def test_attn_decode_split_counters_reset_under_graph_replay():
     assert (first.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("B,L,rows", [(1, 513, 1024), (2, 77, 80), (1, 4096, 4104)])
+def test_attn_decode_reads_cache_views(B, L, rows):
+    """k / v as row-prefix views of [B, Hkv, rows, D] cache buffers (the kv_cache mode) are read
+    in place: the same result, bit for bit, as on contiguous copies."""
+    g = torch.Generator(device="cuda").manual_seed(L)
+    q = torch.randn(B, 32, 1, 128, device="cuda", generator=g)
+    kb = torch.randn(B, 8, rows, 128, device="cuda", generator=g).half()
+    vb = torch.randn(B, 8, rows, 128, device="cuda", generator=g).half()
+    k, v = kb[:, :, :L], vb[:, :, :L]
+    assert qlin._cache_head_stride(k, v) == rows * 128
+    mask = torch.zeros(B, 1, 1, L, device="cuda", dtype=torch.float16)
+    got = qlin.attn_decode(q, k, v, mask, math.sqrt(128))
+    ref = qlin.attn_decode(q, k.contiguous(), v.contiguous(), mask, math.sqrt(128))
+    assert torch.equal(got, ref)
+
+
 def test_attn_decode_rejects_unsupported():
     q = torch.randn(1, 32, 1, 64, device="cuda")
     k = torch.randn(1, 8, 10, 64, device="cuda").half()
@@ -108,6 +124,53 @@ def test_layer_decode_kernel_matches_torch_path():
         got = layer(x, attention_mask=mask, position_ids=pos, past_key_value=past)[0]
     rel = ((got.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
     assert rel < 2e-3, rel
+
+
+def test_layer_kv_cache_mode_matches_cat():
+    """fuse_packed_projections(kv_cache=True): a prefill then decode steps with use_cache append
+    into the module's cache buffers (qlin_rope_kv_f16) instead of torch.cat — identical hidden
+    states and identical past_key_value contents at every step."""
+    from transformers import LlamaConfig
+    from models.int_llama_layer import QuantLlamaDecoderLayer
+    from models.quant_llama import quant_args, random_llama_layer
+    from quant.utils import pack_quant_linears
+    cfg = LlamaConfig(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
+                      num_key_value_heads=2, num_hidden_layers=1, vocab_size=100,
+                      max_position_embeddings=2048, rms_norm_eps=1e-5, rope_theta=500000.0)
+    layers = []
+    for kv in (False, True):
+        layer = QuantLlamaDecoderLayer(cfg, random_llama_layer(cfg, 5, "cuda", torch.float16),
+                                       quant_args(4, 128))
+        layer.half()
+        layer.smooth_and_quant_inplace()
+        layer.register_scales_and_zeros()
+        pack_quant_linears(layer)
+        layer.fuse_packed_projections(kv_cache=kv)
+        layers.append(layer)
+    gen = torch.Generator(device="cuda").manual_seed(2)
+    T0, steps = 300, 4
+    xs = torch.randn(1, T0 + steps, 1024, device="cuda", generator=gen).half()
+    pasts = [None, None]
+    with torch.no_grad():
+        for i in range(steps + 1):
+            lo, hi = (0, T0) if i == 0 else (T0 + i - 1, T0 + i)
+            x = xs[:, lo:hi]
+            L = hi
+            mask = torch.zeros(1, 1, hi - lo, L, device="cuda", dtype=torch.float16)
+            if i == 0:
+                mask[0, 0] = torch.triu(torch.full((T0, T0), torch.finfo(torch.float16).min,
+                                                   device="cuda"), 1).half()
+            pos = torch.arange(lo, hi, device="cuda")[None]
+            outs = []
+            for j, layer in enumerate(layers):
+                o = layer(x, attention_mask=mask, position_ids=pos, past_key_value=pasts[j],
+                          use_cache=True)
+                outs.append(o[0])
+                pasts[j] = o[-1]
+            assert torch.equal(outs[0], outs[1]), i
+            assert torch.equal(pasts[0][0], pasts[1][0]) and torch.equal(pasts[0][1], pasts[1][1]), i
+    # the kv_cache layer's past is a view of its own buffer (no per-step copy of the cache)
+    assert pasts[1][0].data_ptr() == layers[1].self_attn._kv[0].data_ptr()
 
 
 def _causal_mask(B, S, L, dtype=torch.float16, pad=None):

@@ -86,12 +86,19 @@ def test_rmsnorm_kernel_matches_mirror(rows, H):
     assert (diff > 0).float().mean().item() < 0.02
 
 
-@pytest.mark.parametrize("B,S,strided", [(1, 1, True), (1, 37, True), (3, 5, False), (2, 64, True)])
+@pytest.mark.parametrize("B,S,strided", [(1, 1, True), (1, 37, True), (3, 5, False), (2, 64, True),
+                                         (2, 9, "odd")])
 def test_rope_kernel_bit_exact(B, S, strided):
+    """Row kernel (aligned rows) and, for "odd" (rows starting at an odd element, not 8-B
+    aligned), the per-element kernel: both bit-exact with the reference's apply_rotary_pos_emb."""
     from models.int_llama_layer import LlamaRotaryEmbedding437, apply_rotary_pos_emb
     Hq, Hkv, D = 8, 2, 128
     rs = np.random.RandomState(B * 100 + S)
-    qkv = t((rs.randn(B, S, (Hq + 2 * Hkv) * D) * 2).astype(np.float16))
+    qkv = t((rs.randn(B, S, (Hq + 2 * Hkv) * D + 1) * 2).astype(np.float16))
+    if strided == "odd":
+        qkv = qkv[..., 1:]
+    else:
+        qkv = qkv[..., :-1]
     q, k, _ = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
     if not strided:
         q, k = q.contiguous(), k.contiguous()
@@ -106,6 +113,34 @@ def test_rope_kernel_bit_exact(B, S, strided):
     assert got_q.dtype == torch.float32 and got_k.dtype == torch.float16
     assert torch.equal(got_q, ref_q.contiguous())
     assert torch.equal(got_k, ref_k.contiguous())
+
+
+@pytest.mark.parametrize("B,S,kv0,rows", [(1, 1, 0, 8), (1, 1, 511, 512), (2, 7, 20, 64),
+                                          (3, 1, 33, 40)])
+def test_rope_kv_appends_into_cache(B, S, kv0, rows):
+    """qlin_rope_kv_f16 = qlin_rope_f16 + the reference's torch.cat of the KV cache: the rotated
+    k and the v rows land at cache rows kv0 .. kv0 + S - 1 bit for bit; no other row changes."""
+    from models.int_llama_layer import LlamaRotaryEmbedding437
+    Hq, Hkv, D = 8, 2, 128
+    rs = np.random.RandomState(B * 1000 + S + kv0)
+    qkv = t((rs.randn(B, S, (Hq + 2 * Hkv) * D) * 2).astype(np.float16))
+    q, k, v = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
+    rot = LlamaRotaryEmbedding437(D, 1024, 500000.0, device="cuda").half()
+    cos, sin = rot.cos_cached.float().contiguous(), rot.sin_cached.float().contiguous()
+    pos = torch.stack([torch.arange(S) + kv0 + b for b in range(B)]).cuda()
+    kc = t(rs.randn(B, Hkv, rows, D).astype(np.float16))
+    vc = t(rs.randn(B, Hkv, rows, D).astype(np.float16))
+    kc0, vc0 = kc.clone(), vc.clone()
+    got_q = qlin.rope_kv(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, kv0)
+    ref_q, ref_k = qlin.rope(q, k, cos, sin, pos, Hq, Hkv, D)
+    assert torch.equal(got_q, ref_q)
+    assert torch.equal(kc[:, :, kv0:kv0 + S], ref_k)
+    assert torch.equal(vc[:, :, kv0:kv0 + S], v.reshape(B, S, Hkv, D).transpose(1, 2))
+    keep = torch.ones(rows, dtype=torch.bool)
+    keep[kv0:kv0 + S] = False
+    assert torch.equal(kc[:, :, keep], kc0[:, :, keep]) and torch.equal(vc[:, :, keep], vc0[:, :, keep])
+    with pytest.raises(ValueError):
+        qlin.rope_kv(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, rows - S + 1)
 
 
 @pytest.mark.parametrize("M", (1, 2, 5, 16, 33, 200))

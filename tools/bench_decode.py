@@ -50,10 +50,13 @@ def main():
     mask = torch.zeros(1, 1, 1, a.kv + 1, device=dev, dtype=torch.float16)
     pos = torch.tensor([[a.kv]], device=dev)
 
+    cache = {"use": False}
+
     def step():
         h = x
         for layer, pkv in zip(st.layers, past):
-            h = layer(h, attention_mask=mask, position_ids=pos, past_key_value=pkv)[0]
+            h = layer(h, attention_mask=mask, position_ids=pos, past_key_value=pkv,
+                      use_cache=cache["use"])[0]
         return h
 
     def timed():
@@ -84,6 +87,13 @@ def main():
     for layer in st.layers:
         layer.fuse_packed_projections()
     res["packed_fused_us"], y_fu = timed()
+    # + the KV append into preallocated caches (kv_cache mode: RoPE writes the new k / v rows in
+    # place of the reference's two torch.cat copies of the cache)
+    for i, layer in enumerate(st.layers):
+        layer.fuse_packed_projections(kv_cache=True)
+        past[i] = layer.self_attn.adopt_kv_cache(past[i])
+    cache["use"] = True
+    res["packed_fused_kv_cache_us"], y_kv = timed()
     params = sum(m.in_features * m.out_features for l in st.layers for m in l.modules()
                  if hasattr(m, "qweight") and m.__class__.__name__ == "QuantLinear") / a.layers
     wbytes = params * 0.5 + params / 128 * 3
@@ -97,7 +107,10 @@ def main():
            # order differs from the bmm), so the comparison is a relative error, not equality
            "rel_err_fused_vs_unfused": float((y_fu.float() - y_pk.float()).abs().max()
                                              / y_pk.float().abs().max()),
-           "est_32_layer_token_ms": round(res["packed_fused_us"] * 32 / 1e3, 3)}
+           "fused_kv_cache_weight_GBps": round(wbytes / res["packed_fused_kv_cache_us"] / 1e3, 1),
+           "kv_cache_equal_to_cat": bool(torch.equal(y_kv, y_fu)),
+           "est_32_layer_token_ms": round(res["packed_fused_us"] * 32 / 1e3, 3),
+           "est_32_layer_token_ms_kv_cache": round(res["packed_fused_kv_cache_us"] * 32 / 1e3, 3)}
     print(json.dumps(out))
 
 
