@@ -42,7 +42,10 @@ constexpr int kMaxL = 4096;
 constexpr int kSub = 64;         // positions per pass (8 lanes x 16 dims per K row)
 constexpr int kMaxChunk = 512;   // scores of one chunk live in LDS: 512 x 8 fp32 = 16 KB
 constexpr int kMaxSplit = kMaxL / kSub;
-constexpr int kTargetBlocks = 1024;
+#ifndef ATTN_TARGET_BLOCKS  // dev sweeps (tools/dev/Makefile libattnT<N>.so)
+#define ATTN_TARGET_BLOCKS 1024
+#endif
+constexpr int kTargetBlocks = ATTN_TARGET_BLOCKS;
 
 struct Split {
   int chunk, S;

@@ -36,6 +36,8 @@
 // is not read at all.  Query row i sits at key position L - S + i (a cached prefix of L - S keys
 // precedes the window).
 #include "qlin_common.h"
+
+#include <type_traits>
 #include "../../include/qlin_gfx950.h"
 
 namespace {
@@ -45,6 +47,12 @@ constexpr int kKB = 64;       // keys per block
 constexpr int kKS = kD + 8;   // K row stride in LDS (halves): 272 B, conflict-free row reads
 constexpr int kVS = kD + 16;  // V row stride (halves): 288 B, conflict-free transposed reads
 constexpr int kMaxG = 8;      // query heads per KV head
+constexpr float kLog2e = 1.4426950408889634f;
+#ifndef AP_LAZY  // dev switch (tools/dev/Makefile libap<N>.so): 0 = rescale on every new maximum
+#define AP_LAZY 1
+#endif
+// the reference point moves when the row max passes it by this (ln 8: p 2^12 < 2^15)
+constexpr float kLazy = AP_LAZY ? 2.0794415416798357f : 0.f;
 
 struct PrefillArgs {
   const float* q;      // [B, Hq, S, D]
@@ -132,7 +140,11 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   const int nkb = (kend + kKB - 1) / kKB;
 
   // q as fp16 pairs, the B operand of S^T = K Q^T: lane (n, j), d-step t holds
-  // q[row0 + n][32 t + 8 j .. + 7]
+  // q[row0 + n][32 t + 8 j .. + 7], scaled by 2^8 (taken back exactly from every score) so the lo
+  // halves of small elements stay out of the fp16 subnormals.  Only a power of two: q pre-scaled
+  // by log2(e) / sqrt(d) (scores straight in exp2 units) measured 1e-5 relative output errors
+  // against 3e-7 (tools/dev/ap_num.py).
+  const float qscale = 256.f;
   qlin::h8 qh[4], ql[4];
   {
     const float* qp = a.q + (((int64_t)b * a.Hq + hq) * S + min(row, S - 1)) * kD + 8 * j;
@@ -143,7 +155,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         _Float16 h, l;
-        split16(e < 4 ? x0[e] : x1[e - 4], h, l);
+        split16((e < 4 ? x0[e] : x1[e - 4]) * qscale, h, l);
         qh[t][e] = h;
         ql[t][e] = l;
       }
@@ -153,7 +165,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   f4v o[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) o[c] = f4v{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;  // running max / sum of the lane's row
+  // running reference point m and sum l of 2^12 exp(s - m) over the lane's row
+  const float sinv = a.inv * (1.f / 256.f);  // exact: 1 / 256 is a power of two
+  float m = -INFINITY, l = 0.f;
 
   const _Float16* kbase = a.k + ((int64_t)b * a.Hkv + hkv) * L * kD;
   const _Float16* vbase = a.v + ((int64_t)b * a.Hkv + hkv) * L * kD;
@@ -221,45 +235,65 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
         sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[t], sc[sb], 0, 0, 0);
         sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[t], sc[sb], 0, 0, 0);
       }
-    // scale, mask, clamp (the reference's order); keys past L, and in the pure causal pattern keys
-    // past the row's diagonal, drop out (-inf: exp() gives the reference's exact 0)
+    // scores: the reference's x 1 / sqrt(d) (x the fp32 reciprocal, as torch divides by a scalar;
+    // the 2^-8 folded in is exact), + mask and clamp at finfo(fp32).min; keys past L, and in the
+    // pure causal pattern keys past the row's diagonal, drop out (-inf: exp gives the reference's
+    // exact 0)
     float mloc = -INFINITY;
+    auto finish_scores = [&](auto CHK_) {
+      constexpr bool CHK = decltype(CHK_)::value;
 #pragma unroll
-    for (int sb = 0; sb < 4; ++sb)
+      for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 4; ++e) {
 #pragma clang fp contract(off)
-        const int kk = k0 + 16 * sb + 4 * j + e;
-        float sv = sc[sb][e] * a.inv;
-        if constexpr (GMASK) {
-          sv = sv + mc[sb][e];
-          sv = (sv != sv) ? sv : fmaxf(sv, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
+          float sv = sc[sb][e] * sinv;
+          if constexpr (GMASK) {
+            sv = sv + mc[sb][e];
+            sv = (sv != sv) ? sv : fmaxf(sv, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
+          }
+          if constexpr (CHK) {
+            const int kk = k0 + 16 * sb + 4 * j + e;
+            const bool open = kk < L && (a.causal != 2 || kk <= off + row);
+            sv = open ? sv : -INFINITY;
+          }
+          sc[sb][e] = sv;
+          mloc = fmaxf(mloc, sv);
         }
-        const bool open = kk < L && (a.causal != 2 || kk <= off + row);
-        sv = open ? sv : -INFINITY;
-        sc[sb][e] = sv;
-        mloc = fmaxf(mloc, sv);
-      }
-    // online softmax over the row's 64 keys (its 16 values on this lane, x 4 lane groups)
+    };
+    // per-key checks only on blocks that reach past L or (pure causal pattern) past a diagonal
+    if (k0 + kKB > L || (a.causal == 2 && k0 + kKB - 1 > off + row0))  // wave-uniform
+      finish_scores(std::true_type{});
+    else
+      finish_scores(std::false_type{});
+    // online softmax over the row's 64 keys (its 16 values on this lane, x 4 lane groups); the
+    // reference point m moves only when the row maximum passes it by more than ln 8 (lazy
+    // rescale: the 2^12-scaled probabilities stay below 2^15, inside fp16, and the O / l rescale
+    // of every key block is skipped once the maxima settle); exp(x) = exp2(x log2(e)) on the
+    // hardware exp2 (v_exp_f32) with arguments near 0 for the dominant keys
     mloc = fmaxf(mloc, xshfl16(mloc));
     mloc = fmaxf(mloc, xshfl32(mloc));
     const float mn = fmaxf(m, mloc);
-    const float alpha = (mn == -INFINITY) ? 1.f : expf(m - mn);
-    m = mn;
+    if (__builtin_amdgcn_ballot_w64(mn > m + kLazy)) {  // wave-uniform branch
+      const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m - mn) * kLog2e);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[c] *= alpha;
+    }
+    const float mref = (m == -INFINITY) ? 0.f : m;
     float rs = 0.f;
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = (mn == -INFINITY) ? 0.f : expf(sc[sb][e] - mn);
-        sc[sb][e] = pv * 4096.f;  // x 2^12: the fp16 pair of a small P stays out of the subnormals
+        const float pv = __builtin_amdgcn_exp2f((sc[sb][e] - mref) * kLog2e) * 4096.f;
+        sc[sb][e] = pv;
         rs += pv;
       }
     rs += xshfl16(rs);
     rs += xshfl32(rs);
-    l = l * alpha + rs;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) o[c] *= alpha;
+    l += rs;
     // O^T += V^T P^T: key step t (32 keys) in slot order 32 t + 4 j + e, then 32 t + 16 + 4 j + e —
     // P^T is the S^T fragments of sub-blocks 2t, 2t + 1 as they stand; V^T by transposed reads of
     // the row-major V tile (lane 4 q + p of group j: key 32 t [+ 16] + 4 j + q, d 16 c + 4 p)
@@ -286,9 +320,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   }
 
   if (!wave_rows || row >= S) return;
-  // O / (l 2^12) -> out[b][row][hq][16 c + 4 j .. + 3] (the layer's transpose(1, 2) layout;
-  // fp16 = its .to(fp16))
-  const float rl = l * 4096.f;
+  // O / l -> out[b][row][hq][16 c + 4 j .. + 3] (the layer's transpose(1, 2) layout; fp16 = its
+  // .to(fp16))
+  const float rl = l;
   const int64_t base = (((int64_t)b * S + row) * a.Hq + hq) * kD + 4 * j;
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
