@@ -115,8 +115,13 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n = lane & 15, j = lane >> 4;
   const int RB = 64 >> a.lhw;  // query rows per block (16 per wave sub-block)
-  // heaviest (last) row blocks first: causal work grows with the row index
-  int bid = blockIdx.x;
+  // XCD-aware order: dispatch deals block b to XCD b % 8, so with the grid a multiple of 8 XCD x
+  // takes the contiguous logical range [x N / 8, (x + 1) N / 8) — whole (b, KV head) units, whose
+  // K / V (1 MB per KV head at L = 2048) then stay in that XCD's L2 instead of every XCD
+  // streaming every head's K / V; within it the heaviest (last) row blocks first (causal work
+  // grows with the row index)
+  const int nblk = gridDim.x;
+  int bid = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
   const int rb = a.nrb - 1 - bid % a.nrb;
   bid /= a.nrb;
   const int G = a.Hq / a.Hkv;
