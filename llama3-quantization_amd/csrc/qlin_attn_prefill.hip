@@ -51,8 +51,8 @@ constexpr float kLog2e = 1.4426950408889634f;
 #ifndef AP_LAZY  // dev switch (tools/dev/Makefile libap<N>.so): 0 = rescale on every new maximum
 #define AP_LAZY 1
 #endif
-// the reference point moves when the row max passes it by this (ln 8: p 2^12 < 2^15)
-constexpr float kLazy = AP_LAZY ? 2.0794415416798357f : 0.f;
+// the reference point moves when the row max passes it by this (exp2 units: p 2^12 < 2^15)
+constexpr float kLazy = AP_LAZY ? 3.f : 0.f;
 
 struct PrefillArgs {
   const float* q;      // [B, Hq, S, D]
@@ -102,8 +102,40 @@ __device__ __forceinline__ uint2 tr_read(const _Float16* p) {
   return __builtin_bit_cast(uint2, v);
 }
 
-__device__ __forceinline__ float xshfl16(float v) { return __shfl_xor(v, 16); }
-__device__ __forceinline__ float xshfl32(float v) { return __shfl_xor(v, 32); }
+// max / sum over lanes n, n + 16, n + 32, n + 48 (the 4 lane groups holding one query row): two
+// v_permlane*_swap VALU exchanges instead of two LDS round trips (ds_bpermute).  Inline asm: with
+// both operands the same value, hipcc (ROCm 7.2) folds the builtin's two results into one
+// (tools/dev/probe/permlane.hip); the s_nop covers the VALU-write -> permlane-read hazard.
+__device__ __forceinline__ void swap32(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void swap16(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ float groups_max(float v) {
+  float x = v, y = v;
+  swap32(x, y);  // x = v[l % 32], y = v[l % 32 + 32]
+  v = fmaxf(x, y);
+  x = v;
+  y = v;
+  swap16(x, y);  // x, y = the even / odd 16-lane row of the pair
+  return fmaxf(x, y);
+}
+__device__ __forceinline__ float groups_sum(float v) {
+  float x = v, y = v;
+  swap32(x, y);
+  v = x + y;
+  x = v;
+  y = v;
+  swap16(x, y);
+  return x + y;
+}
+
+// p 2^12 as an unevaluated fp16 pair (the scaling is exact; hi + lo within 2^-22 relative)
+__device__ __forceinline__ void split_p(float p, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)(p * 4096.f);
+  lo = (_Float16)__builtin_fmaf(p, 4096.f, -(float)hi);  // exact in fp32, one fp16 rounding
+}
 
 // GMASK: the mask values are read (any mask but the pure causal pattern)
 template <bool GMASK>
@@ -170,8 +202,10 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   f4v o[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) o[c] = f4v{0.f, 0.f, 0.f, 0.f};
-  // running reference point m and sum l of 2^12 exp(s - m) over the lane's row
+  // running reference point m (exp2 units) of the lane's row and sum l of exp2(t - m) over the
+  // lane's keys of it
   const float sinv = a.inv * (1.f / 256.f);  // exact: 1 / 256 is a power of two
+  const float tinv = sinv * kLog2e;
   float m = -INFINITY, l = 0.f;
 
   const _Float16* kbase = a.k + ((int64_t)b * a.Hkv + hkv) * L * kD;
@@ -240,10 +274,12 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
         sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[t], sc[sb], 0, 0, 0);
         sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[t], sc[sb], 0, 0, 0);
       }
-    // scores: the reference's x 1 / sqrt(d) (x the fp32 reciprocal, as torch divides by a scalar;
-    // the 2^-8 folded in is exact), + mask and clamp at finfo(fp32).min; keys past L, and in the
-    // pure causal pattern keys past the row's diagonal, drop out (-inf: exp gives the reference's
-    // exact 0)
+    // scores in exp2 units t = s log2(e): s = the reference's x 1 / sqrt(d) (x the fp32
+    // reciprocal, as torch divides by a scalar; the 2^-8 is exact), with a mask + mask and the
+    // clamp at finfo(fp32).min (clamped again after x log2(e), so a fully masked row stays
+    // uniform as in the reference); without a mask one multiply by log2(e) / (256 sqrt(d)).  Keys
+    // past L, and in the pure causal pattern keys past the row's diagonal, drop out (-inf: exp2
+    // gives the reference's exact 0)
     float mloc = -INFINITY;
     auto finish_scores = [&](auto CHK_) {
       constexpr bool CHK = decltype(CHK_)::value;
@@ -252,10 +288,13 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
 #pragma clang fp contract(off)
-          float sv = sc[sb][e] * sinv;
+          float sv;
           if constexpr (GMASK) {
-            sv = sv + mc[sb][e];
-            sv = (sv != sv) ? sv : fmaxf(sv, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
+            sv = sc[sb][e] * sinv + mc[sb][e];
+            sv = (sv != sv) ? sv
+                            : fmaxf(fmaxf(sv, -3.402823466e38f) * kLog2e, -3.402823466e38f);
+          } else {
+            sv = sc[sb][e] * tinv;
           }
           if constexpr (CHK) {
             const int kk = k0 + 16 * sb + 4 * j + e;
@@ -272,33 +311,28 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
     else
       finish_scores(std::false_type{});
     // online softmax over the row's 64 keys (its 16 values on this lane, x 4 lane groups); the
-    // reference point m moves only when the row maximum passes it by more than ln 8 (lazy
-    // rescale: the 2^12-scaled probabilities stay below 2^15, inside fp16, and the O / l rescale
-    // of every key block is skipped once the maxima settle); exp(x) = exp2(x log2(e)) on the
-    // hardware exp2 (v_exp_f32) with arguments near 0 for the dominant keys
-    mloc = fmaxf(mloc, xshfl16(mloc));
-    mloc = fmaxf(mloc, xshfl32(mloc));
+    // reference point m moves only when the row maximum passes it by more than 3 (lazy rescale:
+    // p 2^12 stays below 2^15, inside fp16, and the O / l rescale of every key block is skipped
+    // once the maxima settle); l is kept per lane (the lane's keys) and summed over the row's
+    // lane groups once, at the end
+    mloc = groups_max(mloc);
     const float mn = fmaxf(m, mloc);
     if (__builtin_amdgcn_ballot_w64(mn > m + kLazy)) {  // wave-uniform branch
-      const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m - mn) * kLog2e);
+      const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mn);
       m = mn;
       l *= alpha;
 #pragma unroll
       for (int c = 0; c < 8; ++c) o[c] *= alpha;
     }
     const float mref = (m == -INFINITY) ? 0.f : m;
-    float rs = 0.f;
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = __builtin_amdgcn_exp2f((sc[sb][e] - mref) * kLog2e) * 4096.f;
+        const float pv = __builtin_amdgcn_exp2f(sc[sb][e] - mref);
         sc[sb][e] = pv;
-        rs += pv;
+        l += pv;
       }
-    rs += xshfl16(rs);
-    rs += xshfl32(rs);
-    l += rs;
     // O^T += V^T P^T: key step t (32 keys) in slot order 32 t + 4 j + e, then 32 t + 16 + 4 j + e —
     // P^T is the S^T fragments of sub-blocks 2t, 2t + 1 as they stand; V^T by transposed reads of
     // the row-major V tile (lane 4 q + p of group j: key 32 t [+ 16] + 4 j + q, d 16 c + 4 p)
@@ -308,7 +342,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         _Float16 h, lo;
-        split16(sc[2 * t + (e >> 2)][e & 3], h, lo);
+        split_p(sc[2 * t + (e >> 2)][e & 3], h, lo);
         ph[e] = h;
         pl[e] = lo;
       }
@@ -327,7 +361,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   if (!wave_rows || row >= S) return;
   // O / l -> out[b][row][hq][16 c + 4 j .. + 3] (the layer's transpose(1, 2) layout; fp16 = its
   // .to(fp16))
-  const float rl = l;
+  const float rl = groups_sum(l) * 4096.f;
   const int64_t base = (((int64_t)b * S + row) * a.Hq + hq) * kD + 4 * j;
 #pragma unroll
   for (int c = 0; c < 8; ++c) {

@@ -6,7 +6,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch
 from test_gpu_attn import _ref, _causal_mask
 P, L64 = ctypes.c_void_p, ctypes.c_int64
-B, Hq, Hkv, S, L = 1, 32, 8, 2048, 2048
+B, Hq, Hkv, S, L = 1, 32, 8, int(os.environ.get("S", "2048")), int(os.environ.get("S", "2048"))
 g = torch.Generator(device="cuda").manual_seed(B * 7919 + S * 31 + L)
 q = torch.randn(B, Hq, S, 128, device="cuda", generator=g) * 0.5
 k = torch.randn(B, Hkv, L, 128, device="cuda", generator=g).half()
