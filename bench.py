@@ -306,6 +306,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()  # no rank tears its transport down while a peer is still draining
         dist.destroy_process_group()
 
 

@@ -56,6 +56,9 @@ def _worker(rank, world, port, out_dir):
         torch.save({"logits": logits, "nll": nll, "lo": info.lo, "hi": info.hi},
                    os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
+        # every rank past its last collective before any tears gloo down (a rank destroying its
+        # group while a peer's transport is still draining aborted the peer now and then)
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -78,6 +78,7 @@ def main():
                           "windows": a.windows, "tokens": a.tokens, "ppl": ppl,
                           "ms_per_window": round(dt / a.windows * 1e3, 2),
                           "nll": [round(float(v), 4) for v in nll]}))
+    dist.barrier()  # no rank tears its transport down while a peer is still draining
     dist.destroy_process_group()
 
 
