@@ -179,6 +179,25 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
                        int act_flags, uint16_t* workspace, void* stream);
 
 /*
+ * RMSNorm + packed linear for ONE token row in one launch (the decoder layer's
+ * input_layernorm -> fused q/k/v and post_attention_layernorm -> gate/up at decode; the norm is
+ * OmniLlamaRMSNorm, quant/omni_norm.py:52-63 of the reference): x fp16 [K] is the hidden state
+ * BEFORE the norm, norm_weight fp32 [K] (8-B aligned), eps its variance epsilon; the GEMV blocks
+ * compute mean(x^2) themselves and normalise their x words (weight * (x * rsqrt(mean + eps)),
+ * rounded to fp16) before the dequant-MFMA, then apply `epilogue` as qlin_linear_ep_f16 does.
+ * The sum of squares runs in another order than qlin_rmsnorm_f16's, so a normed value can differ
+ * from that kernel's by an fp16 ulp.  Supported: M == 1 on the fast GEMV path (K % 128 == 0,
+ * group % 128 == 0 or group in {32, 64}, <= 4 weight tiles per wave) —
+ * qlin_rmsnorm_linear_supported() says so (1) or not (0); otherwise QLIN_EINVAL.
+ */
+int qlin_rmsnorm_linear_supported(int64_t M, int64_t N, int64_t K, int bits, int group);
+int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                               const uint16_t* x, const float* norm_weight, float eps,
+                               const uint16_t* bias, const uint16_t* residual, uint16_t* y,
+                               int64_t M, int64_t N, int64_t K, int bits, int group, int epilogue,
+                               void* stream);
+
+/*
  * Fused decode attention (one query token per sequence), for the quantized LLaMA layer's
  * attention core (models/int_llama_layer.py:137-165 of the reference: repeat_kv, fp32 QK^T bmm,
  * / sqrt(head_dim), + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV bmm) on an fp16 K/V

@@ -44,8 +44,14 @@ namespace {
 
 constexpr int kD = 128;       // head_dim
 constexpr int kKB = 64;       // keys per block
-constexpr int kKS = kD + 8;   // K row stride in LDS (halves): 272 B, conflict-free row reads
-constexpr int kVS = kD + 16;  // V row stride (halves): 288 B, conflict-free transposed reads
+#ifndef AP_KPAD  // dev switches (tools/dev/Makefile libap*.so APX=...)
+#define AP_KPAD 8
+#endif
+#ifndef AP_VPAD
+#define AP_VPAD 16
+#endif
+constexpr int kKS = kD + AP_KPAD;  // K row stride in LDS (halves): 272 B, conflict-free row reads
+constexpr int kVS = kD + AP_VPAD;  // V row stride (halves): 288 B, conflict-free transposed reads
 constexpr int kMaxG = 8;      // query heads per KV head
 constexpr float kLog2e = 1.4426950408889634f;
 #ifndef AP_LAZY  // dev switch (tools/dev/Makefile libap<N>.so): 0 = rescale on every new maximum
@@ -103,33 +109,17 @@ __device__ __forceinline__ uint2 tr_read(const _Float16* p) {
 }
 
 // max / sum over lanes n, n + 16, n + 32, n + 48 (the 4 lane groups holding one query row): two
-// v_permlane*_swap VALU exchanges instead of two LDS round trips (ds_bpermute).  Inline asm: with
-// both operands the same value, hipcc (ROCm 7.2) folds the builtin's two results into one
-// (tools/dev/probe/permlane.hip); the s_nop covers the VALU-write -> permlane-read hazard.
-__device__ __forceinline__ void swap32(float& x, float& y) {
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-}
-__device__ __forceinline__ void swap16(float& x, float& y) {
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-}
+// v_permlane*_swap VALU exchanges (qlin_common.h) instead of two LDS round trips (ds_bpermute)
 __device__ __forceinline__ float groups_max(float v) {
   float x = v, y = v;
-  swap32(x, y);  // x = v[l % 32], y = v[l % 32 + 32]
+  qlin::permlane32_swap(x, y);  // x = v[l % 32], y = v[l % 32 + 32]
   v = fmaxf(x, y);
   x = v;
   y = v;
-  swap16(x, y);  // x, y = the even / odd 16-lane row of the pair
+  qlin::permlane16_swap(x, y);  // x, y = the even / odd 16-lane row of the pair
   return fmaxf(x, y);
 }
-__device__ __forceinline__ float groups_sum(float v) {
-  float x = v, y = v;
-  swap32(x, y);
-  v = x + y;
-  x = v;
-  y = v;
-  swap16(x, y);
-  return x + y;
-}
+__device__ __forceinline__ float groups_sum(float v) { return qlin::cols4_sum(v); }
 
 // p 2^12 as an unevaluated fp16 pair (the scaling is exact; hi + lo within 2^-22 relative)
 __device__ __forceinline__ void split_p(float p, _Float16& hi, _Float16& lo) {

@@ -336,6 +336,31 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// v_permlane32_swap / v_permlane16_swap (gfx950): x <-> y exchanges across the wave halves / the
+// odd and even 16-lane rows, VALU only (no LDS round trip).  Inline asm: with both operands the
+// same value, hipcc (ROCm 7.2) folds the builtin's two results into one
+// (tools/dev/probe/permlane.hip); the s_nop covers the VALU-write -> permlane-read hazard.
+// After permlane32_swap(x, y) with x = y = v: x = v[l % 32], y = v[l % 32 + 32]; after
+// permlane16_swap likewise for the even / odd row of each pair of 16-lane rows.
+__device__ __forceinline__ void permlane32_swap(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void permlane16_swap(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+// sum over lanes n, n + 16, n + 32, n + 48 (every lane gets its column's total)
+__device__ __forceinline__ float cols4_sum(float v) {
+  float x = v, y = v;
+  permlane32_swap(x, y);
+  v = x + y;
+  x = v;
+  y = v;
+  permlane16_swap(x, y);
+  return x + y;
+}
+// sum over all 64 lanes, every lane gets it (16-lane rows by DPP, then the row exchanges)
+__device__ __forceinline__ float wave_sum(float v) { return cols4_sum(row16_sum(v)); }
+
 // output epilogues of the packed linear (qlin_linear_ep_f16); the accumulator (+ bias) is first
 // rounded to fp16 exactly as F.linear's output, then
 //   kEpResidual  y = RN16(residual + that)           (the decoder layer's `residual + h`)

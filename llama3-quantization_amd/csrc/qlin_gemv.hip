@@ -381,6 +381,9 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
 //   - all codes of the prefetch window are issued before their (scale, zero) words and x, so the
 //     first tile only waits for its own three loads.
 // ---------------------------------------------------------------------------------------------
+#ifndef GEMV_NRM_XFIRST  // dev switch: the fused norm's x words issued before the codes
+#define GEMV_NRM_XFIRST 1
+#endif
 struct FastArgs {
   const uint32_t* qw;   // row tile 0 of qweight
   const uint32_t* qsz;  // row tile 0 of qsz
@@ -391,14 +394,26 @@ struct FastArgs {
   int M, N, K, Kt, G;
   int W, lw;            // waves per block (power of two), log2 W
   uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
+  const float* nw;      // NRM: RMSNorm weight (fp32 [K]) applied to x first
+  float eps;
 };
 
 // every wave streams at most PF tiles, all of them loaded up front (no refill loop: a launch whose
-// waves need more tiles takes gemv_kernel, whose contiguous tile runs stream better then)
-template <int BITS, int MT, int GPT, int ZM, int EP, int PF>
+// waves need more tiles takes gemv_kernel, whose contiguous tile runs stream better then).
+// NRM (M = 1): x is the decoder layer's hidden state before its RMSNorm (OmniLlamaRMSNorm,
+// quant/omni_norm.py:52-63 of the reference) and the kernel applies the norm itself: each wave
+// sums the squares of the x words it loads anyway (its own tiles; together the waves cover the
+// row once), the block combines the W wave sums through LDS behind a bare s_barrier (no vmcnt
+// drain), and every x word is normalised (weight * (x * rsqrt(mean + eps)), fp32, rounded to fp16
+// as the norm's output) before it is parked.  One launch instead of two (the separate
+// qlin_rmsnorm_f16); the sum of squares runs in another order than that kernel's, so the normed
+// x can differ from it by an fp16 ulp.
+template <int BITS, int MT, int GPT, int ZM, int EP, int PF, bool NRM = false>
 __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
+  __shared__ float nss[NRM ? kMaxWaves : 1];  // NRM: per-wave sums of squares
+  static_assert(!NRM || MT == 1, "the fused RMSNorm serves one token row");
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
@@ -416,11 +431,14 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   };
   WTile<BITS, GPT> wt[PF];
   XRaw<MT> xq[PF];
+  float2 nwv[NRM ? PF : 1];  // NRM: norm weights of the lane's two x halves per tile
   auto load_codes = [&](int u, int kt) { wt[u].pc = load_piece_nt<BITS>(qw + kt * (64 * BITS)); };
-  auto load_rest = [&](int u, int kt) {
+  auto load_sz = [&](int u, int kt) {
     const int g0 = group_of_tile(kt);
 #pragma unroll
     for (int s = 0; s < GPT; ++s) wt[u].sz[s] = sz[(g0 + s) * kTileN];
+  };
+  auto load_x = [&](int u, int kt) {
     const _Float16* p = xr + kt * kTileK;
     if constexpr (MT == 1) {
       xq[u].w[0] = *reinterpret_cast<const uint32_t*>(p);
@@ -432,10 +450,35 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
       xq[u].w[0] = v.x; xq[u].w[1] = v.y; xq[u].w[2] = v.z; xq[u].w[3] = v.w;
     }
   };
+  if constexpr (NRM) {
+#if GEMV_NRM_XFIRST
 #pragma unroll
-  for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
+    for (int u = 0; u < PF; ++u) {
+      load_x(u, kt_of(u));
+      nwv[u] = *reinterpret_cast<const float2*>(a.nw + kt_of(u) * kTileK + 2 * lane);
+    }
 #pragma unroll
-  for (int u = 0; u < PF; ++u) load_rest(u, kt_of(u));
+    for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
+#else
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      load_x(u, kt_of(u));
+      nwv[u] = *reinterpret_cast<const float2*>(a.nw + kt_of(u) * kTileK + 2 * lane);
+    }
+#endif
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_sz(u, kt_of(u));
+  } else {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      load_sz(u, kt_of(u));
+      load_x(u, kt_of(u));
+    }
+  }
   // the epilogue's bias / residual operands, fetched while the weights stream (fetched after the
   // reduction they would cost one more round trip).  Only wave 0's lanes use them, but every wave
   // loads (clamped, L2-resident): a load under a branch is waited for at the branch's join
@@ -449,11 +492,40 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   _Float16 ores = 0;
   if constexpr (EP == kEpResidual) ores = a.res[(int64_t)om * a.N + min(orow, (int64_t)a.N - 1)];
 
+  float rn = 1.f;  // NRM: rsqrt(mean(x^2) + eps)
+  if constexpr (NRM) {
+#pragma clang fp contract(off)
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (u < nts) {  // wave-uniform: slots past the wave's tiles repeat its last tile
+        const h2 v = as_h2(xq[u].w[0]);
+        const float f0 = (float)v.x, f1 = (float)v.y;
+        ss = ss + f0 * f0;
+        ss = ss + f1 * f1;
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) nss[wave] = ss;
+    // a bare s_barrier after the LDS store: __syncthreads() would also drain vmcnt, i.e. wait for
+    // the sz words still in flight; the waves only need each other's sums
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float tot = 0.f;
+    for (int w = 0; w < a.W; ++w) tot += nss[w];
+    rn = rsqrtf(tot / (float)a.K + a.eps);
+  }
+
   const Magics mg = make_magics<BITS>();
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   uint32_t* slot = &xs[wave][0];
   auto tile = [&](int u) {
     h8 xa[4];
+    if constexpr (NRM) {
+#pragma clang fp contract(off)
+      const h2 v = as_h2(xq[u].w[0]);
+      const float n0 = nwv[u].x * ((float)v.x * rn), n1 = nwv[u].y * ((float)v.y * rn);
+      xq[u].w[0] = as_u32(h2{(_Float16)n0, (_Float16)n1});
+    }
     park_x<MT>(xa, xq[u], slot, lane, n_in);
     auto step = [&](auto S_) {
       constexpr int S = decltype(S_)::value;
@@ -608,11 +680,18 @@ bool fast_ok(int M, int K, int group, const Ep& e) {
 
 template <int BITS, int MT, int GPT, int ZM, int EP>
 int launch_fast_t(const FastArgs& a, int Nt, int tpw, hipStream_t st) {
-#define QLIN_GF(PF)                                                                           \
-  hipLaunchKernelGGL((gemv_fast_kernel<BITS, MT, GPT, ZM, EP, PF>), dim3(Nt), dim3(64 * a.W), \
-                     0, st, a)
-  if (tpw <= 2) QLIN_GF(2);
-  else QLIN_GF(4);
+#define QLIN_GF(PF, NR)                                                                      \
+  hipLaunchKernelGGL((gemv_fast_kernel<BITS, MT, GPT, ZM, EP, PF, NR>), dim3(Nt),          \
+                     dim3(64 * a.W), 0, st, a)
+  if constexpr (MT == 1) {
+    if (a.nw) {
+      if (tpw <= 2) QLIN_GF(2, true);
+      else QLIN_GF(4, true);
+      return (int)hipGetLastError();
+    }
+  }
+  if (tpw <= 2) QLIN_GF(2, false);
+  else QLIN_GF(4, false);
 #undef QLIN_GF
   return (int)hipGetLastError();
 }
@@ -633,9 +712,11 @@ bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
 template <int BITS, int MT, int ZM>
 int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                 uint16_t* y, int M, int N, int K, int group, int W, int lw, int tpw,
-                hipStream_t st, const Ep& e) {
+                hipStream_t st, const Ep& e, const float* nw = nullptr, float eps = 0.f) {
   const int Nt = (N + kTileN - 1) / kTileN;
   FastArgs a;
+  a.nw = nw;
+  a.eps = eps;
   a.qw = qw;
   a.qsz = qsz;
   a.x = (const _Float16*)x;
@@ -750,6 +831,57 @@ int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const
     default: QLIN_G(8);
   }
 #undef QLIN_G
+}
+
+namespace {
+// the fused RMSNorm + linear serves one token row on the fast path (M = 1, K % 128 == 0, whole /
+// 32 / 64-wide groups, <= 4 tiles per wave)
+bool rmsnorm_linear_ok(int64_t M, int64_t N, int64_t K, int bits, int group) {
+  if (M != 1 || N < 1 || !valid_layout(N, K, bits, group)) return false;
+  const Ep e{nullptr, kEpNone, ActQ{false, 0, 0, 0.f, 0.f}};
+  int W = 0, lw = 0, tpw = 0;
+  return fast_ok(1, (int)K, group, e) &&
+         fast_geometry((int)((N + kTileN - 1) / kTileN), (int)(K / kTileK), W, lw, tpw);
+}
+}  // namespace
+
+extern "C" int qlin_rmsnorm_linear_supported(int64_t M, int64_t N, int64_t K, int bits,
+                                             int group) {
+  return rmsnorm_linear_ok(M, N, K, bits, group) ? 1 : 0;
+}
+
+extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                                          const uint16_t* x, const float* norm_weight, float eps,
+                                          const uint16_t* bias, const uint16_t* residual,
+                                          uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
+                                          int group, int epilogue, void* stream) {
+  if (!qweight || !qsz || !x || !norm_weight || !y || !rmsnorm_linear_ok(M, N, K, bits, group) ||
+      ((uintptr_t)norm_weight & 7) || ((uintptr_t)x & 3) || !(eps >= 0.f) ||
+      epilogue < kEpNone || epilogue > kEpSiluMul || (epilogue == kEpResidual && !residual) ||
+      (epilogue == kEpSiluMul && N % kTileN))
+    return QLIN_EINVAL;
+  const Ep e{residual, epilogue, ActQ{false, 0, 0, 0.f, 0.f}};
+  hipStream_t st = (hipStream_t)stream;
+  const int n = (int)N, k = (int)K;
+  int W = 0, lw = 0, tpw = 0;
+  fast_geometry((n + kTileN - 1) / kTileN, k / kTileK, W, lw, tpw);
+  const int zm = zero_mode(flags);
+#define QLIN_N(B)                                                                             \
+  return zm == kZFloat                                                                        \
+             ? launch_fast<B, 1, kZFloat>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw, tpw, \
+                                          st, e, norm_weight, eps)                            \
+         : zm == kZWide                                                                       \
+             ? launch_fast<B, 1, kZWide>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw, tpw,  \
+                                         st, e, norm_weight, eps)                             \
+             : launch_fast<B, 1, kZNarrow>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw,     \
+                                           tpw, st, e, norm_weight, eps)
+  switch (bits) {
+    case 2: QLIN_N(2);
+    case 3: QLIN_N(3);
+    case 4: QLIN_N(4);
+    default: QLIN_N(8);
+  }
+#undef QLIN_N
 }
 
 extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,

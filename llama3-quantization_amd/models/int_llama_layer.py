@@ -116,19 +116,31 @@ class QuantLlamaMLP(nn.Module):
             _same_act([self.gate_proj, self.up_proj]) is not None and \
             act_spec(self.down_proj) is not None
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, prenorm=None):
         """``down(act(gate(x)) * up(x))``; with ``residual`` (fused packed mode only) the
-        decoder layer's ``residual + mlp(x)`` is folded into down_proj's epilogue."""
+        decoder layer's ``residual + mlp(x)`` is folded into down_proj's epilogue; ``prenorm``
+        (fused packed mode): x is the hidden state BEFORE that RMSNorm module, applied here — for
+        one token row inside the gate/up launch (qlin.rmsnorm_linear_ep)."""
         if self.fused():
             act = _same_act([self.gate_proj, self.up_proj])
-            if self.gate_up_act is not None:
-                h = self.gate_up_act(x, act)
+            lin = self.gate_up_act if self.gate_up_act is not None else self.gate_up
+            norm = prenorm.fusable(x) if prenorm is not None else None
+            if norm is not None and lin.prenorm_ok(x, act):
+                out = lin.forward_prenorm(x, norm)
             else:
-                gate, up = self.gate_up(x, act)
+                if prenorm is not None:
+                    x = prenorm(x)
+                out = lin(x, act)
+            if self.gate_up_act is not None:
+                h = out
+            else:
+                gate, up = out
                 h = self.act_fn(gate) * up
             if residual is not None:
                 return packed_residual_linear(self.down_proj, h, residual)
             return self.down_proj(h)
+        if prenorm is not None:
+            x = prenorm(x)
         out = self.down_proj(self.act_fn(self.gate_proj(x)) * self.up_proj(x))
         return out if residual is None else residual + out
 
@@ -236,11 +248,20 @@ class QuantLlamaAttention(nn.Module):
                 return False
         return True
 
-    def _project(self, hidden_states):
+    def _project(self, hidden_states, prenorm=None):
+        """q, k, v of the (normed) hidden state; ``prenorm``: hidden_states is the input of that
+        RMSNorm module, applied here — for one token row inside the fused q/k/v launch."""
         if self.qkv is not None:
             act = _same_act([self.q_proj, self.k_proj, self.v_proj])
             if act is not None:
+                norm = prenorm.fusable(hidden_states) if prenorm is not None else None
+                if norm is not None and self.qkv.prenorm_ok(hidden_states, act):
+                    return self.qkv.forward_prenorm(hidden_states, norm)
+                if prenorm is not None:
+                    hidden_states = prenorm(hidden_states)
                 return self.qkv(hidden_states, act)
+        if prenorm is not None:
+            hidden_states = prenorm(hidden_states)
         return self.q_proj(hidden_states), self.k_proj(hidden_states), self.v_proj(hidden_states)
 
     def _rope_cache(self, value_states, kv_seq_len):
@@ -275,12 +296,15 @@ class QuantLlamaAttention(nn.Module):
         output_attentions: bool = False,
         use_cache: bool = False,
         residual: Optional[torch.Tensor] = None,
+        prenorm=None,
     ):
         """``residual`` (fused packed mode, set by the decoder layer): the output is
-        ``residual + o_proj(attn)``, the add folded into o_proj's epilogue."""
+        ``residual + o_proj(attn)``, the add folded into o_proj's epilogue; ``prenorm``: the
+        input_layernorm module, applied to hidden_states here (inside the q/k/v launch for one
+        token row)."""
         bsz, q_len, _ = hidden_states.size()
         act_dtype = hidden_states.dtype
-        q, k, v = self._project(hidden_states)
+        q, k, v = self._project(hidden_states, prenorm)
         value_states = v.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
         kv_seq_len = q_len
         if past_key_value is not None:
@@ -409,17 +433,20 @@ class QuantLlamaDecoderLayer(nn.Module):
         use_cache: Optional[bool] = False,
     ):
         residual = hidden_states
-        hidden_states = self.input_layernorm(hidden_states)
         if self.fused_epilogues and self.mlp.fused():
             # fused packed mode: both residual adds run in the o_proj / down_proj epilogues
-            # (same fp16 arithmetic: RN16(residual + RN16(linear)))
+            # (same fp16 arithmetic: RN16(residual + RN16(linear))), and both RMSNorms are handed
+            # to the q/k/v and gate/up launches (applied inside them for one token row)
             hidden_states, self_attn_weights, present_key_value = self.self_attn(
                 hidden_states=hidden_states, attention_mask=attention_mask,
                 position_ids=position_ids, past_key_value=past_key_value,
-                output_attentions=output_attentions, use_cache=use_cache, residual=residual)
+                output_attentions=output_attentions, use_cache=use_cache, residual=residual,
+                prenorm=self.input_layernorm)
             residual = hidden_states
-            hidden_states = self.mlp(self.post_attention_layernorm(hidden_states), residual=residual)
+            hidden_states = self.mlp(hidden_states, residual=residual,
+                                     prenorm=self.post_attention_layernorm)
         else:
+            hidden_states = self.input_layernorm(hidden_states)
             hidden_states, self_attn_weights, present_key_value = self.self_attn(
                 hidden_states=hidden_states, attention_mask=attention_mask,
                 position_ids=position_ids, past_key_value=past_key_value,

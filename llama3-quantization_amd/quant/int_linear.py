@@ -235,6 +235,19 @@ class FusedPackedLinear(nn.Module):
         else:
             self.bias = None
 
+    def prenorm_ok(self, x, act=(0, 0)):
+        """Whether ``forward_prenorm`` takes this input (one fp16 token row, no act quant)."""
+        return (act == (0, 0) and x.dtype == torch.float16 and x.numel() == self.in_features
+                and qlin.rmsnorm_linear_supported(1, self.out_features, self.in_features,
+                                                  self.wbits, self.group))
+
+    def forward_prenorm(self, x, norm):
+        """``forward(rmsnorm(x))`` in one launch; ``norm`` = (fp32 weight, eps)."""
+        y = qlin.rmsnorm_linear_ep(x.contiguous(), norm[0], norm[1], self.qweight, self.qsz,
+                                   self.bias, self.out_features, self.in_features, self.wbits,
+                                   self.group, self.qflags)
+        return torch.split(y, self.splits, dim=-1)
+
     def forward(self, x, act=(0, 0)):
         """``act``: (act_bits, act_flags) of the members' shared per-token act quantizer."""
         xin = x if x.dtype == torch.float16 else x.to(torch.float16)
@@ -278,6 +291,19 @@ class SiluMulPackedLinear(nn.Module):
             self.register_buffer("bias", torch.stack([gb.view(-1, 8), ub.view(-1, 8)], 1).reshape(-1))
         else:
             self.bias = None
+
+    def prenorm_ok(self, x, act=(0, 0)):
+        """Whether ``forward_prenorm`` takes this input (one fp16 token row, no act quant)."""
+        return (act == (0, 0) and x.dtype == torch.float16 and x.numel() == self.in_features
+                and qlin.rmsnorm_linear_supported(1, 2 * self.out_features, self.in_features,
+                                                  self.wbits, self.group))
+
+    def forward_prenorm(self, x, norm):
+        """``forward(rmsnorm(x))`` in one launch; ``norm`` = (fp32 weight, eps)."""
+        return qlin.rmsnorm_linear_ep(x.contiguous(), norm[0], norm[1], self.qweight, self.qsz,
+                                      self.bias, 2 * self.out_features, self.in_features,
+                                      self.wbits, self.group, self.qflags,
+                                      epilogue=qlin.EP_SILU_MUL)
 
     def forward(self, x, act=(0, 0)):
         xin = x if x.dtype == torch.float16 else x.to(torch.float16)

@@ -61,6 +61,15 @@ class OmniLlamaRMSNorm(nn.Module):
             self._w32 = (w, w._version, w.detach().to(torch.float32).contiguous())
         return self._w32[2]
 
+    def fusable(self, hidden_states):
+        """(fp32 weight, eps) when the next packed linear may apply this norm itself
+        (qlin.rmsnorm_linear_ep: the kernel path, one fp16 token row), else None."""
+        if (self.use_kernel and not self.use_temporary_parameter and self.bias is None
+                and hidden_states.is_cuda and hidden_states.dtype == torch.float16
+                and hidden_states.numel() == hidden_states.shape[-1]):
+            return self._kernel_weight(), self.variance_epsilon
+        return None
+
     def forward(self, hidden_states):
         if (self.use_kernel and not self.use_temporary_parameter and self.bias is None
                 and hidden_states.is_cuda and hidden_states.dtype == torch.float16

@@ -51,6 +51,9 @@ SIGNATURES = {
                            _i),
     "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),
     "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
+    "qlin_rmsnorm_linear_supported": ([_l, _l, _l, _i, _i], _i),
+    "qlin_rmsnorm_linear_ep_f16": ([_p, _p, _i, _p, _p, ctypes.c_float, _p, _p, _p, _l, _l, _l,
+                                    _i, _i, _i, _p], _i),
     "qlin_rope_kv_f16": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _p, _l, _l, _l, _l,
                           _i, _i, _i, _p], _i),
     "qlin_attn_scores_f32": ([_p, _p, _i, _l, _l, _l, _l, _l, ctypes.c_float, _p], _i),
@@ -349,6 +352,40 @@ def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NON
                                            _ptr(residual), _ptr(y), M, N, K, bits, group,
                                            epilogue, act_bits, act_flags, _ptr(ws), _stream(x))
     _check(rc, "qlin_linear_ep_f16")
+    return y
+
+
+def rmsnorm_linear_supported(M, N, K, bits, group):
+    """Whether ``rmsnorm_linear_ep`` takes this shape (one token row on the fast GEMV path)."""
+    return bool(load_library().qlin_rmsnorm_linear_supported(M, N, K, bits, group))
+
+
+def rmsnorm_linear_ep(x, norm_weight, eps, qweight, qsz, bias, N, K, bits, group, flags=0,
+                      epilogue=EP_NONE, residual=None):
+    """``qlin_rmsnorm_linear_ep_f16``: ``linear_ep(rmsnorm(x))`` for one token row in ONE launch —
+    x fp16 [.., K] is the hidden state BEFORE the RMSNorm (norm_weight fp32 [K], eps), which the
+    GEMV applies to its x words itself (the sum of squares in another order than ``rmsnorm``:
+    the normed x can differ from it by an fp16 ulp)."""
+    _dev(x, qweight, qsz, bias, residual, norm_weight)
+    if x.dtype != torch.float16 or norm_weight.dtype != torch.float32:
+        raise ValueError("rmsnorm_linear_ep takes fp16 x and an fp32 norm weight")
+    if x.shape[-1] != K or norm_weight.numel() != K:
+        raise ValueError(f"input / norm weight do not have {K} features")
+    if bias is not None and (bias.dtype != torch.float16 or bias.numel() != N):
+        raise ValueError("bias must be fp16 [N]")
+    _check_packed(qweight, qsz, N, K, bits, group)
+    M = x.numel() // K
+    if not rmsnorm_linear_supported(M, N, K, bits, group):
+        raise ValueError(f"rmsnorm_linear_ep: unsupported shape M={M} N={N} K={K} g{group}")
+    ny = N // 2 if epilogue == EP_SILU_MUL else N
+    y = torch.empty(*x.shape[:-1], ny, dtype=torch.float16, device=x.device)
+    if epilogue == EP_RESIDUAL:
+        if residual is None or residual.dtype != torch.float16 or residual.shape != y.shape:
+            raise ValueError(f"residual must be fp16 {tuple(y.shape)}")
+    rc = load_library().qlin_rmsnorm_linear_ep_f16(
+        _ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(norm_weight), float(eps), _ptr(bias),
+        _ptr(residual), _ptr(y), M, N, K, bits, group, epilogue, _stream(x))
+    _check(rc, "qlin_rmsnorm_linear_ep_f16")
     return y
 
 

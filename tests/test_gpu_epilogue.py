@@ -202,3 +202,42 @@ def test_attn_scores_pass_bit_exact(mask):
     got = qlin.attn_scores_(w.clone(), m, math.sqrt(128))
     assert torch.equal(torch.nan_to_num(got, nan=7.0), torch.nan_to_num(ref, nan=7.0))
     assert torch.isnan(got[0, 0, 0, 0])
+
+
+@pytest.mark.parametrize("N,K,bits,group,ep", [(6144, 4096, 4, 128, "none"),
+                                               (4096, 4096, 4, 128, "residual"),
+                                               (2 * 2816, 1024, 4, 128, "silu"),
+                                               (1024, 2048, 3, 64, "none"),
+                                               (512, 1024, 2, 32, "residual"),
+                                               (28672, 4096, 4, 128, "silu")])
+def test_rmsnorm_linear_matches_two_launches(N, K, bits, group, ep):
+    """qlin_rmsnorm_linear_ep_f16 (one token row: the RMSNorm applied by the GEMV to its own x
+    words, the statistics shared through LDS) against the two launches it replaces (qlin_rmsnorm_f16,
+    then the packed linear): the norm's sum of squares runs in another order, so a normed x value
+    can move one fp16 ulp — outputs within 2e-3 of max |y| and nearly all bit-equal."""
+    qw, qsz, fl = _packed(N, K, 21, bits, group)
+    rs = np.random.RandomState(N + K)
+    x = t((rs.randn(1, 1, K) * 3).astype(np.float16))
+    w = torch.tensor((1 + 0.1 * rs.randn(K)).astype(np.float32), device="cuda")
+    epc = {"none": qlin.EP_NONE, "residual": qlin.EP_RESIDUAL, "silu": qlin.EP_SILU_MUL}[ep]
+    ny = N // 2 if ep == "silu" else N
+    res = t(rs.randn(1, 1, ny).astype(np.float16)) if ep == "residual" else None
+    assert qlin.rmsnorm_linear_supported(1, N, K, bits, group)
+    xn = qlin.rmsnorm(x, w, 1e-5)
+    ref = qlin.linear_ep(xn, qw, qsz, None, N, K, bits, group, fl, epilogue=epc, residual=res)
+    got = qlin.rmsnorm_linear_ep(x, w, 1e-5, qw, qsz, None, N, K, bits, group, fl, epilogue=epc,
+                                 residual=res)
+    assert got.shape == ref.shape
+    scale = ref.float().abs().max().item()
+    assert (got.float() - ref.float()).abs().max().item() <= 2e-3 * scale
+    assert (got == ref).float().mean().item() > 0.9
+
+
+def test_rmsnorm_linear_rejects_unsupported():
+    qw, qsz, fl = _packed(256, 1024, 5)
+    w = torch.ones(1024, device="cuda")
+    assert not qlin.rmsnorm_linear_supported(2, 256, 1024, 4, 128)  # one token row only
+    assert not qlin.rmsnorm_linear_supported(1, 256, 1000, 4, 40)   # K % 128
+    x2 = t(np.ones((2, 1024), np.float16))
+    with pytest.raises(ValueError):
+        qlin.rmsnorm_linear_ep(x2, w, 1e-5, qw, qsz, None, 256, 1024, 4, 128, fl)
