@@ -221,6 +221,23 @@ int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const
                      void* stream);
 
 /*
+ * qlin_rope_kv_f16 + qlin_attn_decode in one launch, for one query token per sequence with a KV
+ * cache that has room for the new row: q / k / v are the step's projection rows BEFORE RoPE (fp16,
+ * row b at q + b * q_row_stride, Hq resp. Hkv heads of D), cos / sin / position_ids as for
+ * qlin_rope_f16; the caches fp16 [B, Hkv, rows, D] with head stride kv_head_stride (>= L * D)
+ * hold rows 0 .. L - 2 and receive the rotated k and the v row at L - 1 from this launch, which
+ * then attends over all L rows (mask fp16 [B, L] or NULL).  Same arithmetic as the two launches
+ * (bit-identical output and cache rows); partials / counters as qlin_attn_decode.
+ */
+int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+                          int64_t k_row_stride, const uint16_t* v, int64_t v_row_stride,
+                          const float* cos_cache, const float* sin_cache, int64_t cache_rows,
+                          const int64_t* position_ids, int64_t pos_batch_stride, uint16_t* k_cache,
+                          uint16_t* v_cache, int64_t kv_head_stride, const uint16_t* mask,
+                          void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int D,
+                          float scale_div, float* partials, int32_t* counters, void* stream);
+
+/*
  * Fused prefill attention (many query tokens per sequence): the same attention core as
  * qlin_attn_decode — repeat_kv, fp32 QK^T, / sqrt(head_dim) (as torch: x the fp32 reciprocal),
  * + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV (models/int_llama_layer.py:137-165 of

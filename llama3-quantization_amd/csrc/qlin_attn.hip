@@ -89,14 +89,37 @@ __device__ __forceinline__ float h2f(uint32_t w, int hi) {
 
 // partials: [o fp32 B*Hkv*S*GRP*D][m, l fp32 B*Hkv*S*GRP*2]; counters: int32 [B*Hkv], zero
 
-template <int GRP>
+// ROPE: the step's RoPE and KV-cache append inside the attention launch (qlin_attn_decode_rope):
+// q / k / v are the fused q/k/v projection's fp16 rows before RoPE; every block rotates the q
+// rows of its query heads (qlin_rope_f16's fp32 arithmetic), and the block whose chunk holds the
+// new cache row L - 1 rotates k (fp16 arithmetic), writes k and v into the cache row for later
+// steps and uses them in place of that row's loads (the cache row is written by this launch)
+struct RopeIn {
+  const _Float16* q16;
+  int64_t q_rs;
+  const _Float16* k16;
+  int64_t k_rs;
+  const _Float16* v16;
+  int64_t v_rs;
+  const float* cosc;
+  const float* sinc;
+  int64_t cache_rows;
+  const int64_t* pos;
+  int64_t pos_bs;
+  _Float16* kc;  // the caches k / v (writable views of the same buffers)
+  _Float16* vc;
+};
+
+template <int GRP, bool ROPE = false>
 __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
     const float* __restrict__ q, const _Float16* __restrict__ k, const _Float16* __restrict__ v,
     const _Float16* __restrict__ mask, void* __restrict__ out, int out_f16, int Hq, int Hkv,
     int L, int64_t kv_hs, int chunk,
     int S, float scale_div, int* __restrict__ counters, float* __restrict__ part_o,
-    float* __restrict__ part_ml) {
+    float* __restrict__ part_ml, const RopeIn ri) {
   __shared__ float qs[GRP][kD];
+  __shared__ __attribute__((aligned(16))) _Float16 knew[ROPE ? kD : 8];  // ROPE: the new k row
+  __shared__ __attribute__((aligned(16))) _Float16 vnew[ROPE ? kD : 8];  // ... and v row
   __shared__ float sc[kMaxChunk][GRP];     // scores, then probabilities (position-major)
   __shared__ float po[kWaves][GRP * kD];   // per-wave P V (and merge) partial sums
   __shared__ float cm[GRP], cl[GRP];       // chunk max / sum; merged denominators
@@ -142,8 +165,40 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   load_k(0);
   load_v(0);
 
-  const float* qb = q + ((int64_t)b * Hq + (int64_t)hk * GRP) * kD;
-  for (int i = tid; i < GRP * kD; i += kThreads) qs[i / kD][i % kD] = qb[i];
+  const bool has_new = ROPE && split == S - 1;  // this block's chunk holds the new row L - 1
+  if constexpr (ROPE) {
+#pragma clang fp contract(off)
+    const int64_t p = min(max(ri.pos[(int64_t)b * ri.pos_bs], (int64_t)0), ri.cache_rows - 1);
+    const float* cr = ri.cosc + p * kD;
+    const float* sr = ri.sinc + p * kD;
+    constexpr int half = kD / 2;
+    for (int i = tid; i < GRP * kD; i += kThreads) {
+      const int g = i / kD, d = i % kD;
+      const _Float16* qr = ri.q16 + (int64_t)b * ri.q_rs + (int64_t)(hk * GRP + g) * kD;
+      const float c = (float)(_Float16)cr[d], sn = (float)(_Float16)sr[d];
+      const float x = (float)qr[d];
+      const float rx = d < half ? -(float)qr[d + half] : (float)qr[d - half];
+      qs[g][d] = x * c + rx * sn;  // fp32, each op rounded once (qlin_rope_f16)
+    }
+    if (has_new && tid < kD) {
+      const int d = tid;
+      const _Float16* kr = ri.k16 + (int64_t)b * ri.k_rs + (int64_t)hk * kD;
+      const float c = (float)(_Float16)cr[d], sn = (float)(_Float16)sr[d];
+      const float x = (float)kr[d];
+      const float rx = d < half ? -(float)kr[d + half] : (float)kr[d - half];
+      const float a0 = (float)(_Float16)(x * c), b0 = (float)(_Float16)(rx * sn);
+      const _Float16 kn = (_Float16)(a0 + b0);  // fp16 ops, as the reference's k path
+      const _Float16 vn = ri.v16[(int64_t)b * ri.v_rs + (int64_t)hk * kD + d];
+      knew[d] = kn;
+      vnew[d] = vn;
+      const int64_t row = (int64_t)bh * kv_hs + (int64_t)(L - 1) * kD + d;
+      ri.kc[row] = kn;  // the cache row, for the following steps
+      ri.vc[row] = vn;
+    }
+  } else {
+    const float* qb = q + ((int64_t)b * Hq + (int64_t)hk * GRP) * kD;
+    for (int i = tid; i < GRP * kD; i += kThreads) qs[i / kD][i % kD] = qb[i];
+  }
   __syncthreads();
 
   // scores (the next pass's K rows are in flight while this pass computes)
@@ -155,6 +210,10 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
       kc[u][0] = kw[u][0];
       kc[u][1] = kw[u][1];
       mc[u] = mv[u];
+      if (has_new && t0 + tb + 32 * u + tl == L - 1) {  // the new row: written by this launch
+        kc[u][0] = *reinterpret_cast<const u32x4*>(&knew[16 * sub]);
+        kc[u][1] = *reinterpret_cast<const u32x4*>(&knew[16 * sub + 8]);
+      }
     }
     if (tb + kSub < n) load_k(tb + kSub);
 #pragma unroll
@@ -221,7 +280,11 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
     for (int tb = 0; tb < n; tb += kSub) {
       uint32_t vc[kSub / kWaves];
 #pragma unroll
-      for (int u = 0; u < kSub / kWaves; ++u) vc[u] = vw[u];
+      for (int u = 0; u < kSub / kWaves; ++u) {
+        vc[u] = vw[u];
+        if (has_new && t0 + tb + wave + kWaves * u == L - 1)
+          vc[u] = *reinterpret_cast<const uint32_t*>(&vnew[2 * lane]);
+      }
       if (tb + kSub < n) load_v(tb + kSub);
 #pragma unroll
       for (int u = 0; u < kSub / kWaves; ++u) {
@@ -325,6 +388,33 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   if (tid == 0) counters[bh] = 0;  // ready for the next launch (graph replay)
 }
 
+int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
+                  void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int64_t kv_hs,
+                  float scale_div, float* part_o, float* part_ml, int32_t* counters,
+                  const Split& sp, hipStream_t st, const RopeIn& ri) {
+  const dim3 grid((unsigned)(B * Hkv), (unsigned)sp.S);
+  const int grp = Hq / Hkv;
+#define QLIN_A(G, R)                                                                          \
+  hipLaunchKernelGGL((attn_decode_kernel<G, R>), grid, dim3(kThreads), 0, st, q,              \
+                     (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,        \
+                     out_dtype == QLIN_F16, Hq, Hkv, (int)L, kv_hs, sp.chunk, sp.S, scale_div,  \
+                     (int*)counters, part_o, part_ml, ri)
+#define QLIN_AR(G)                \
+  if (ri.q16) QLIN_A(G, true);    \
+  else QLIN_A(G, false);          \
+  break
+  switch (grp) {
+    case 1: QLIN_AR(1);
+    case 2: QLIN_AR(2);
+    case 4: QLIN_AR(4);
+    case 8: QLIN_AR(8);
+    default: return QLIN_EINVAL;
+  }
+#undef QLIN_AR
+#undef QLIN_A
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L) {
@@ -359,20 +449,42 @@ extern "C" int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_
     part_o = partials;
     part_ml = part_o + heads * sp.S * grp * kD;
   }
-  const dim3 grid((unsigned)heads, (unsigned)sp.S);
-  hipStream_t st = (hipStream_t)stream;
-#define QLIN_A(G)                                                                             \
-  hipLaunchKernelGGL((attn_decode_kernel<G>), grid, dim3(kThreads), 0, st, q,                 \
-                     (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,        \
-                     out_dtype == QLIN_F16, Hq,                                                 \
-                     Hkv, (int)L, kv_hs, sp.chunk, sp.S, scale_div, (int*)counters, part_o, part_ml)
-  switch (grp) {
-    case 1: QLIN_A(1); break;
-    case 2: QLIN_A(2); break;
-    case 4: QLIN_A(4); break;
-    case 8: QLIN_A(8); break;
-    default: return QLIN_EINVAL;
+  return launch_decode(q, k, v, mask, out, out_dtype, B, Hq, Hkv, L, kv_hs, scale_div, part_o,
+                       part_ml, counters, sp, (hipStream_t)stream, RopeIn{});
+}
+
+extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+                                     int64_t k_row_stride, const uint16_t* v,
+                                     int64_t v_row_stride, const float* cos_cache,
+                                     const float* sin_cache, int64_t cache_rows,
+                                     const int64_t* position_ids, int64_t pos_batch_stride,
+                                     uint16_t* k_cache, uint16_t* v_cache, int64_t kv_head_stride,
+                                     const uint16_t* mask, void* out, int out_dtype, int64_t B,
+                                     int Hq, int Hkv, int64_t L, int D, float scale_div,
+                                     float* partials, int32_t* counters, void* stream) {
+  if (!q || !k || !v || !cos_cache || !sin_cache || !position_ids || !k_cache || !v_cache ||
+      !out || (out_dtype != QLIN_F32 && out_dtype != QLIN_F16) || B < 0 || Hq <= 0 ||
+      Hkv <= 0 || Hq % Hkv || L <= 0 || L > kMaxL || D != kD || B * Hkv > 0x7fffffff ||
+      q_row_stride < (int64_t)Hq * kD || k_row_stride < (int64_t)Hkv * kD ||
+      v_row_stride < (int64_t)Hkv * kD || cache_rows <= 0 || pos_batch_stride < 0 ||
+      kv_head_stride < L * kD || kv_head_stride % 8)
+    return QLIN_EINVAL;
+  const int grp = Hq / Hkv;
+  if (grp > kMaxGroup) return QLIN_EINVAL;
+  if (B == 0) return QLIN_OK;
+  const Split sp = choose_split(B, Hkv, L);
+  if (sp.S > kMaxSplit || sp.S > 65535) return QLIN_EINVAL;
+  const int64_t heads = B * Hkv;
+  float *part_o = nullptr, *part_ml = nullptr;
+  if (sp.S > 1) {
+    if (!partials || !counters) return QLIN_EINVAL;
+    part_o = partials;
+    part_ml = part_o + heads * sp.S * grp * kD;
   }
-#undef QLIN_A
-  return (int)hipGetLastError();
+  const RopeIn ri{(const _Float16*)q, q_row_stride, (const _Float16*)k, k_row_stride,
+                  (const _Float16*)v, v_row_stride, cos_cache, sin_cache, cache_rows,
+                  position_ids, pos_batch_stride, (_Float16*)k_cache, (_Float16*)v_cache};
+  return launch_decode(nullptr, k_cache, v_cache, mask, out, out_dtype, B, Hq, Hkv, L,
+                       kv_head_stride, scale_div, part_o, part_ml, counters, sp,
+                       (hipStream_t)stream, ri);
 }

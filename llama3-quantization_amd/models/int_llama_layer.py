@@ -221,22 +221,28 @@ class QuantLlamaAttention(nn.Module):
         self._kv = (kb, vb)
         return (kb[:, :, :L0], vb[:, :, :L0])
 
-    def _rope_append(self, q, k, v, cos_c, sin_c, position_ids, past, bsz, q_len):
-        """kv_cache mode: RoPE + the cache append in one launch (qlin_rope_kv_f16); returns
-        (query_states, key_states, value_states) with k / v as views of the cache buffers."""
+    def _cache_for(self, past, bsz, q_len, device):
+        """kv_cache mode: the cache buffers with ``past`` as their row prefix and room for
+        ``q_len`` more rows (adopting ``past`` by one copy when it is not such a view)."""
         H, D = self.num_key_value_heads, self.head_dim
         L0 = past[0].shape[-2] if past is not None else 0
-        need = L0 + q_len
         buf = self._kv
-        inplace = (past is not None and buf is not None and need <= buf[0].shape[2]
+        inplace = (past is not None and buf is not None and L0 + q_len <= buf[0].shape[2]
                    and past[0].data_ptr() == buf[0].data_ptr()
                    and past[1].data_ptr() == buf[1].data_ptr()
                    and tuple(past[0].shape) == (bsz, H, L0, D)
                    and tuple(past[1].shape) == (bsz, H, L0, D)
                    and past[0].stride() == buf[0].stride() and past[1].stride() == buf[1].stride())
         if not inplace:
-            self.adopt_kv_cache(past, rows=need, batch=bsz, device=q.device)
-            buf = self._kv
+            self.adopt_kv_cache(past, rows=L0 + q_len, batch=bsz, device=device)
+        return self._kv, L0
+
+    def _rope_append(self, q, k, v, cos_c, sin_c, position_ids, past, bsz, q_len):
+        """kv_cache mode: RoPE + the cache append in one launch (qlin_rope_kv_f16); returns
+        (query_states, key_states, value_states) with k / v as views of the cache buffers."""
+        H, D = self.num_key_value_heads, self.head_dim
+        buf, L0 = self._cache_for(past, bsz, q_len, q.device)
+        need = L0 + q_len
         query_states = qlin.rope_kv(q, k, v, cos_c, sin_c, position_ids, self.num_heads, H, D,
                                     buf[0], buf[1], L0)
         return query_states, buf[0][:, :, :need], buf[1][:, :, :need]
@@ -315,8 +321,24 @@ class QuantLlamaAttention(nn.Module):
         if self.rope_kernel and q.dtype == torch.float16 and q.is_cuda:
             # one launch: reshape/transpose, q -> fp32, cos/sin slice + cast, apply_rotary_pos_emb
             cos_c, sin_c = self._rope_cache(value_states, kv_seq_len)
-            if self.kv_cache and (use_cache or past_key_value is not None) and \
-                    (past_key_value is None or past_key_value[0].dtype == torch.float16):
+            kv_mode = self.kv_cache and (use_cache or past_key_value is not None) and \
+                (past_key_value is None or past_key_value[0].dtype == torch.float16)
+            if (kv_mode and q_len == 1 and self.decode_kernel and not output_attentions
+                    and self._attn_bypassed() and self.head_dim == qlin.ATTN_D
+                    and kv_seq_len <= qlin.ATTN_MAX_L
+                    and self.num_heads // self.num_key_value_heads in (1, 2, 4, 8)
+                    and (attention_mask is None or (attention_mask.dtype == torch.float16
+                                                    and attention_mask.shape[-2] == 1))):
+                # one launch: RoPE, the cache append and the decode attention
+                buf, L0 = self._cache_for(past_key_value, bsz, 1, q.device)
+                attn_output = qlin.attn_decode_rope(
+                    q, k, v, cos_c, sin_c, position_ids, self.num_heads, self.num_key_value_heads,
+                    self.head_dim, buf[0], buf[1], L0, attention_mask, math.sqrt(self.head_dim),
+                    out_dtype=act_dtype if act_dtype == torch.float16 else torch.float32)
+                past_key_value = (buf[0][:, :, :L0 + 1], buf[1][:, :, :L0 + 1]) if use_cache else None
+                attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
+                return self._out(attn_output, residual), None, past_key_value
+            if kv_mode:
                 # ... plus the cache append (kv_cache mode)
                 query_states, key_states, value_states = self._rope_append(
                     q, k, v, cos_c, sin_c, position_ids, past_key_value, bsz, q_len)

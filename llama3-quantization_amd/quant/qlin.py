@@ -51,6 +51,8 @@ SIGNATURES = {
                            _i),
     "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),
     "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
+    "qlin_attn_decode_rope": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _p, _p, _i,
+                               _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p], _i),
     "qlin_rmsnorm_linear_supported": ([_l, _l, _l, _i, _i], _i),
     "qlin_rmsnorm_linear_ep_f16": ([_p, _p, _i, _p, _p, ctypes.c_float, _p, _p, _p, _l, _l, _l,
                                     _i, _i, _i, _p], _i),
@@ -607,6 +609,59 @@ def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32):
                               B, Hq, Hkv, L, D, hs, float(scale_div), _ptr(part), _ptr(cnt),
                               _stream(q))
     _check(rc, "qlin_attn_decode")
+    return out
+
+
+def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim,
+                     k_cache, v_cache, kv0, mask, scale_div, out_dtype=torch.float32):
+    """``qlin_attn_decode_rope``: ``rope_kv`` + ``attn_decode`` in one launch for one new token:
+    q [B, 1, Hq*D], k / v [B, 1, Hkv*D] fp16 row-strided views (before RoPE); k_cache / v_cache
+    fp16 [B, Hkv, rows, D] contiguous buffers holding rows 0 .. kv0 - 1, row kv0 written here;
+    mask fp16 [B, 1, 1, kv0 + 1] or None -> [B, Hq, 1, D] (out_dtype), bit-identical to the two
+    launches."""
+    for t_ in (q, k, v):
+        if _rows(t_) is None:
+            raise ValueError("attn_decode_rope takes row-strided [B, 1, H*D] q / k / v")
+    _on_gpu(q, k, v, cos_cache, sin_cache, position_ids, k_cache, v_cache, mask)
+    B = q.shape[0]
+    if q.shape[1] != 1 or head_dim != ATTN_D or n_heads % n_kv_heads or \
+            n_heads // n_kv_heads not in (1, 2, 4, 8):
+        raise ValueError("attn_decode_rope: one token, head_dim 128, GQA group 1/2/4/8")
+    if q.dtype != torch.float16 or k.dtype != torch.float16 or v.dtype != torch.float16 or \
+            k_cache.dtype != torch.float16 or v_cache.dtype != torch.float16:
+        raise ValueError("attn_decode_rope takes fp16 q / k / v and caches")
+    if not (k_cache.is_contiguous() and v_cache.is_contiguous()) or k_cache.shape != v_cache.shape \
+            or tuple(k_cache.shape[:2]) != (B, n_kv_heads) or k_cache.shape[3] != head_dim:
+        raise ValueError("attn_decode_rope takes contiguous [B, Hkv, rows, D] caches of one shape")
+    L = kv0 + 1
+    if kv0 < 0 or L > k_cache.shape[2] or L > ATTN_MAX_L:
+        raise ValueError(f"cache rows {k_cache.shape[2]} cannot take row {kv0}")
+    if cos_cache.dtype != torch.float32 or not cos_cache.is_contiguous() or \
+            sin_cache.dtype != torch.float32 or not sin_cache.is_contiguous():
+        raise ValueError("rope takes contiguous fp32 cos / sin caches")
+    pos, pbs = _pos_ids(position_ids, B, 1)
+    m = None
+    if mask is not None:
+        if mask.dtype != torch.float16 or mask.shape[-1] != L or mask.shape[-2] != 1:
+            raise ValueError("attn_decode_rope: mask fp16 [B, 1, 1, L]")
+        m = mask.reshape(B, L).contiguous() if mask.shape[0] == B else \
+            mask.expand(B, 1, 1, L).reshape(B, L).contiguous()
+    out = torch.empty(B, n_heads, 1, head_dim, dtype=out_dtype, device=q.device)
+    lib = load_library()
+    nbytes = lib.qlin_attn_decode_partials_bytes(B, n_heads, n_kv_heads, L)
+    if nbytes < 0:
+        raise ValueError("attn_decode_rope: unsupported shapes")
+    part = cnt = None
+    if nbytes:
+        part = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
+        cnt = _attn_counters(q.device, B * n_kv_heads)
+    rows = k_cache.shape[2]
+    rc = lib.qlin_attn_decode_rope(
+        _ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(v), _rows(v), _ptr(cos_cache),
+        _ptr(sin_cache), cos_cache.shape[0], _ptr(pos), pbs, _ptr(k_cache), _ptr(v_cache),
+        rows * head_dim, _ptr(m), _ptr(out), _dtcode(out), B, n_heads, n_kv_heads, L, head_dim,
+        float(scale_div), _ptr(part), _ptr(cnt), _stream(q))
+    _check(rc, "qlin_attn_decode_rope")
     return out
 
 

@@ -87,6 +87,37 @@ def test_attn_decode_reads_cache_views(B, L, rows):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("B,Hq,Hkv,kv0,rows,masked", [(1, 32, 8, 512, 1024, True),
+                                                     (1, 32, 8, 0, 256, False),
+                                                     (2, 16, 4, 77, 80, True),
+                                                     (1, 8, 1, 4095, 4096, False),
+                                                     (3, 8, 8, 300, 512, True)])
+def test_attn_decode_rope_equals_two_launches(B, Hq, Hkv, kv0, rows, masked):
+    """qlin_attn_decode_rope (RoPE + KV append + decode attention in one launch) = qlin_rope_kv_f16
+    then qlin_attn_decode, bit for bit: output and the written cache row."""
+    from models.int_llama_layer import LlamaRotaryEmbedding437
+    D = 128
+    g = torch.Generator(device="cuda").manual_seed(kv0 + 7 * B)
+    qkv = (torch.randn(B, 1, (Hq + 2 * Hkv) * D, device="cuda", generator=g) * 2).half()
+    q, k, v = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
+    rot = LlamaRotaryEmbedding437(D, 8192, 500000.0, device="cuda").half()
+    cos, sin = rot.cos_cached.float().contiguous(), rot.sin_cached.float().contiguous()
+    pos = torch.full((B, 1), kv0, device="cuda", dtype=torch.int64)
+    kc = torch.randn(B, Hkv, rows, D, device="cuda", generator=g).half()
+    vc = torch.randn(B, Hkv, rows, D, device="cuda", generator=g).half()
+    kc2, vc2 = kc.clone(), vc.clone()
+    mask = None
+    if masked:
+        mask = torch.zeros(B, 1, 1, kv0 + 1, device="cuda", dtype=torch.float16)
+        mask[..., : kv0 // 4] = torch.finfo(torch.float16).min
+    got = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, kv0, mask,
+                                math.sqrt(D))
+    qr = qlin.rope_kv(q, k, v, cos, sin, pos, Hq, Hkv, D, kc2, vc2, kv0)
+    ref = qlin.attn_decode(qr, kc2[:, :, :kv0 + 1], vc2[:, :, :kv0 + 1], mask, math.sqrt(D))
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    assert torch.equal(got, ref)
+
+
 def test_attn_decode_rejects_unsupported():
     q = torch.randn(1, 32, 1, 64, device="cuda")
     k = torch.randn(1, 8, 10, 64, device="cuda").half()
