@@ -44,14 +44,6 @@ namespace {
 
 constexpr int kD = 128;       // head_dim
 constexpr int kKB = 64;       // keys per block
-#ifndef AP_KPAD  // dev switches (tools/dev/Makefile libap*.so APX=...)
-#define AP_KPAD 8
-#endif
-#ifndef AP_VPAD
-#define AP_VPAD 16
-#endif
-constexpr int kKS = kD + AP_KPAD;  // K row stride in LDS (halves): 272 B, conflict-free row reads
-constexpr int kVS = kD + AP_VPAD;  // V row stride (halves): 288 B, conflict-free transposed reads
 constexpr int kMaxG = 8;      // query heads per KV head
 constexpr float kLog2e = 1.4426950408889634f;
 #ifndef AP_LAZY  // dev switch (tools/dev/Makefile libap<N>.so): 0 = rescale on every new maximum
@@ -128,10 +120,29 @@ __device__ __forceinline__ void split_p(float p, _Float16& hi, _Float16& lo) {
 }
 
 // GMASK: the mask values are read (any mask but the pure causal pattern)
+// K / V tiles in LDS: [64 keys][256 B] unpadded, 16-B chunk c of key row r stored at chunk
+// c ^ swz(r): the K row reads (16 rows, one chunk each) and the transposed V reads (4 rows x 32 B
+// per 16 lanes, 8 rows per 32) both hit distinct banks
+__device__ __forceinline__ int swz(int r) { return ((r & 7) << 1) | ((r >> 3) & 1); }
+
+// a buffer descriptor over [p, p + bytes) from readfirstlane'd inputs (provably wave-uniform, so
+// no waterfall loop around the buffer ops)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t srd(const void* p, uint32_t bytes) {
+  const uint64_t ad = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ad);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(ad >> 32));
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)nb,
+                                           0x00020000);
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr;
+
 template <bool GMASK>
 __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) {
-  __shared__ __attribute__((aligned(16))) _Float16 ks[kKB * kKS];  // K [64 keys][128 d], 17,408 B
-  __shared__ __attribute__((aligned(16))) _Float16 vs[kKB * kVS];  // V [64 keys][128 d], 18,432 B
+  // two stages of K and V [64 keys][128 d] (16 KB each): key block kb + 1 streams in by LDS-DMA
+  // while block kb computes
+  __shared__ __attribute__((aligned(1024))) unsigned char kvs[2][2][kKB * kD * 2];
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -207,16 +218,27 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
                                                     (int64_t)min(row, S - 1) * L) * esz;
   }
 
-  // the next block's K / V rows (and the lane's mask values), in registers while a block computes
-  u4v kr[4], vr[4];
-  float mk[4][4];
-  auto fetch = [&](int k0) {
+  // K / V staging by LDS-DMA (buffer_load ... lds, 16 B per lane): wave w moves tile rows
+  // 16 w .. 16 w + 15 of K and of V (4 instructions each, 1 KB = 4 rows apiece); lane l writes
+  // row 4 i + l / 16 at chunk l % 16, i.e. it fetches the chunk (l % 16) ^ swz(row).  Rows past L
+  // fall outside the descriptors and read 0 (their scores are dropped).
+  const __amdgpu_buffer_rsrc_t rk = srd(kbase, (uint32_t)((int64_t)L * kD * 2));
+  const __amdgpu_buffer_rsrc_t rv = srd(vbase, (uint32_t)((int64_t)L * kD * 2));
+  uint32_t dvo[4];  // the lane's byte offset inside a key block, per instruction
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // chunk c = tid + 256 u -> key c / 16, d 8 (c % 16)
-      const int c = tid + 256 * u, key = c >> 4, d8 = (c & 15) * 8;
-      const int64_t r = (int64_t)min(k0 + key, L - 1) * kD + d8;
-      kr[u] = *reinterpret_cast<const u4v*>(kbase + r);
-      vr[u] = *reinterpret_cast<const u4v*>(vbase + r);
+  for (int i = 0; i < 4; ++i) {
+    const int r = 16 * wave + 4 * i + (lane >> 4);
+    dvo[i] = (uint32_t)(r * (kD * 2) + 16 * ((lane & 15) ^ swz(r)));
+  }
+  float mk[4][4];  // GMASK: the next block's mask values of the lane
+  auto fetch = [&](int stage, int k0) {
+    unsigned char* kd = &kvs[stage][0][0] + wave * 4096;
+    unsigned char* vd = &kvs[stage][1][0] + wave * 4096;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t vo = dvo[i] + (uint32_t)k0 * (kD * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_ptr)(kd + 1024 * i), 16, vo, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_ptr)(vd + 1024 * i), 16, vo, 0, 0, 0);
     }
     if constexpr (GMASK) {
 #pragma unroll
@@ -229,17 +251,19 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
         }
     }
   };
-  fetch(0);
+  // the lane's fragment offsets (loop-invariant): K row 16 sb + n chunk 4 t + j; V^T rows
+  // 32 t + 4 j + n / 4 (+ 16), bytes 8 (n & 3) + 32 c
+  const int fk = swz(n);
+  const int vrow = 4 * j + (n >> 2);
+  const int fv = swz(vrow);
+  fetch(0, 0);
 
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * kKB;
-    __syncthreads();  // every wave is done with the previous block's K / V
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = tid + 256 * u, key = c >> 4, d8 = (c & 15) * 8;
-      *reinterpret_cast<u4v*>(ks + key * kKS + d8) = kr[u];
-      *reinterpret_cast<u4v*>(vs + key * kVS + d8) = vr[u];
-    }
+    // block kb has landed for every wave (each drains its own DMA), and every wave is done with
+    // block kb - 1, whose stage the next fetch overwrites
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
     float mc[4][4];
     if constexpr (GMASK) {
 #pragma unroll
@@ -247,9 +271,10 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
 #pragma unroll
         for (int e = 0; e < 4; ++e) mc[sb][e] = mk[sb][e];
     }
-    __syncthreads();
-    fetch(k0 + kKB);  // lands while this block computes (past the last block: clamped, unused)
+    if (kb + 1 < nkb) fetch((kb + 1) & 1, k0 + kKB);  // lands while this block computes
     if (!wave_rows || k0 >= kend_w) continue;  // wave-uniform; the wave still stages and syncs
+    const unsigned char* ks = &kvs[kb & 1][0][0];
+    const unsigned char* vs = &kvs[kb & 1][1][0];
 
     // S^T = K Q^T (fp32 accumulate of k q_hi + k q_lo): lane (n, j) of sub-block sb holds
     // S[row][k0 + 16 sb + 4 j + e]
@@ -260,7 +285,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int sb = 0; sb < 4; ++sb) {
-        const qlin::h8 kf = *reinterpret_cast<const qlin::h8*>(ks + (16 * sb + n) * kKS + 32 * t + 8 * j);
+        const qlin::h8 kf = *reinterpret_cast<const qlin::h8*>(
+            ks + (16 * sb + n) * (kD * 2) + 16 * ((4 * t + j) ^ fk));
         sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[t], sc[sb], 0, 0, 0);
         sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[t], sc[sb], 0, 0, 0);
       }
@@ -336,11 +362,12 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
         ph[e] = h;
         pl[e] = lo;
       }
-      const _Float16* vr0 = vs + (32 * t + 4 * j + (n >> 2)) * kVS + 4 * (n & 3);
+      const unsigned char* vr0 = vs + (32 * t + vrow) * (kD * 2) + 8 * (n & 1);
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const uint2 lo4 = tr_read(vr0 + 16 * c);
-        const uint2 hi4 = tr_read(vr0 + 16 * kVS + 16 * c);
+        const int ch = (2 * c + ((n & 3) >> 1)) ^ fv;
+        const uint2 lo4 = tr_read(reinterpret_cast<const _Float16*>(vr0 + 16 * ch));
+        const uint2 hi4 = tr_read(reinterpret_cast<const _Float16*>(vr0 + 16 * (kD * 2) + 16 * ch));
         const qlin::h8 vf = __builtin_bit_cast(qlin::h8, make_uint4(lo4.x, lo4.y, hi4.x, hi4.y));
         o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, ph, o[c], 0, 0, 0);
         o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pl, o[c], 0, 0, 0);
