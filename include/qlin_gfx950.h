@@ -147,7 +147,8 @@ int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, con
 
 /*
  * Output columns per block that qlin_gemm_f16 picks for an M x N launch on the current device
- * (128, 256, 384 or 512; 128 = the 64-row x 128-column block for small grids), or -1 for invalid
+ * (128, 256, 384 or 512; 128 = the 64-row x 128-column block for small grids, 255 = the 64-row x
+ * 256-column block for grids a little larger), or -1 for invalid
  * arguments.  Introspection for tests and tools; no reference counterpart.
  */
 int qlin_gemm_block_cols(int64_t M, int64_t N, int bits);

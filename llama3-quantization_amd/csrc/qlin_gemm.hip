@@ -49,9 +49,10 @@ typedef __attribute__((address_space(1))) void* gbl_ptr;
 // chosen per launch by pick_bn (whole rounds of blocks over the CUs).
 // BN_ = 128: the 64 x 128 block for grids that leave most CUs idle at 128 x 256 (fewer rows
 // and columns per block, the same k order per output).
-template <int BITS, int BN_, int NW = 4> struct Cfg {
+// HALF: 64-row blocks at width 256 (two fit a CU; pick_bn)
+template <int BITS, int BN_, int NW = 4, bool HALF = false> struct Cfg {
   static constexpr int BN = BN_;
-  static constexpr int BM = BN_ == 128 ? 64 : 128;  // block rows
+  static constexpr int BM = (BN_ == 128 || HALF) ? 64 : 128;  // block rows
   static constexpr int THREADS = 64 * NW;
   static constexpr int WGN = NW, WGM = 1;  // the waves side by side in N: B dequantized once
   static constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -89,12 +90,12 @@ __device__ __forceinline__ int gemm_group_of(const GemmGeo& g, int k) {
 }
 
 // one k-tile's DMA into stage buffer `st`: x tile, packed codes, (scale, zero) words
-template <int BITS, int WN_, int GPT, int NW>
+template <int BITS, int WN_, int GPT, int NW, bool HALF = false>
 __device__ __forceinline__ void load_stage(unsigned char* st, const GemmGeo& g, int kt,
                                            const _Float16* __restrict__ x,
                                            const uint32_t* __restrict__ qw,
                                            const uint32_t* __restrict__ qsz) {
-  using C = Cfg<BITS, WN_, NW>;
+  using C = Cfg<BITS, WN_, NW, HALF>;
   // x: BM rows x 16 chunks; one instruction = 4 rows (1 KB); wave w owns rows [BM/NW w, +BM/NW).
   // Rows >= M re-read row M-1 and k >= K re-reads the row's last chunk: those C rows are never
   // stored and those k-steps are skipped.
@@ -150,10 +151,11 @@ __device__ __forceinline__ void read_a(h8 (&a)[MB], const unsigned char* as, int
 
 // FULL: every k-tile lies inside K (K % 128 == 0, chosen per launch): straight-line k-steps
 // (ABL bit 2, lab only: the raw packed words stand in for the dequantized B fragment)
-template <int BITS, int WN_, int GPT, int ZM, bool FULL, int NW, int ABL = 0>
-__device__ __forceinline__ void compute_stage(const unsigned char* st, const GemmGeo& g, int kt,
-                                              f4 (&acc)[Cfg<BITS, WN_, NW>::MB][Cfg<BITS, WN_, NW>::NB]) {
-  using C = Cfg<BITS, WN_, NW>;
+template <int BITS, int WN_, int GPT, int ZM, bool FULL, int NW, int ABL = 0, bool HALF = false>
+__device__ __forceinline__ void compute_stage(
+    const unsigned char* st, const GemmGeo& g, int kt,
+    f4 (&acc)[Cfg<BITS, WN_, NW, HALF>::MB][Cfg<BITS, WN_, NW, HALF>::NB]) {
+  using C = Cfg<BITS, WN_, NW, HALF>;
   constexpr int MB = C::MB, NB = C::NB, WM = C::WM;
   const int wm = g.wave / C::WGN, wn = g.wave % C::WGN;
   const int lane = g.lane, n_in = lane & 15, q = lane >> 4;
@@ -300,14 +302,15 @@ __device__ __forceinline__ void store_tile(const f4 (&acc)[MB][NB], int64_t M, i
 }
 
 // ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
-// the DMA after the first k-tile, bit 2 the dequant VALU; the library instantiates ABL = 0 only
-template <int BITS, int WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4>
+// the DMA after the first k-tile, bit 2 the dequant VALU; the library instantiates ABL = 0 only.
+// HALF: 64-row blocks (Cfg)
+template <int BITS, int WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4, bool HALF = false>
 __global__ __launch_bounds__(64 * NW) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
     int64_t M, int N, int K, int group, uint32_t gmagic, int tiles_m, int tiles_n,
     const _Float16* __restrict__ res, int ep) {
-  using C = Cfg<BITS, WN_, NW>;
+  using C = Cfg<BITS, WN_, NW, HALF>;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * C::STAGE];
   GemmGeo g;
   g.M = M;
@@ -336,15 +339,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
 #pragma unroll
     for (int j = 0; j < C::NB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  load_stage<BITS, WN_, GPT, NW>(smem, g, 0, x, qw, qsz);
+  load_stage<BITS, WN_, GPT, NW, HALF>(smem, g, 0, x, qw, qsz);
   for (int kt = 0; kt < g.Kt; ++kt) {
     // stage kt has landed for every wave, and every wave is done reading stage kt - 1
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
     __syncthreads();
     if (!(ABL & 2) && kt + 1 < g.Kt)
-      load_stage<BITS, WN_, GPT, NW>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
+      load_stage<BITS, WN_, GPT, NW, HALF>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
     if (!(ABL & 1))
-      compute_stage<BITS, WN_, GPT, ZM, KFULL, NW, ABL>(smem + (kt & 1) * C::STAGE, g, kt, acc);
+      compute_stage<BITS, WN_, GPT, ZM, KFULL, NW, ABL, HALF>(smem + (kt & 1) * C::STAGE, g, kt, acc);
   }
 
   const int wm = g.wave / C::WGN, wn = g.wave % C::WGN;
@@ -357,15 +360,17 @@ uint32_t group_magic(int group) {
   return (uint32_t)(((1ull << 31) + d - 1) / d);
 }
 
-template <int BITS, int WN_, int GPT, int ZM>
+template <int BITS, int WN_, int GPT, int ZM, bool HALF = false>
 int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
-  const int tiles_n = (N + Cfg<BITS, WN_>::BN - 1) / Cfg<BITS, WN_>::BN;
-  const int64_t tiles_m = (M + Cfg<BITS, WN_>::BM - 1) / Cfg<BITS, WN_>::BM;
+  using C = Cfg<BITS, WN_, kWaves, HALF>;
+  const int tiles_n = (N + C::BN - 1) / C::BN;
+  const int64_t tiles_m = (M + C::BM - 1) / C::BM;
   const int64_t blocks = tiles_m * tiles_n;
   if (blocks > 0x7fffffff) return QLIN_EINVAL;
 #define QLIN_GL(KF)                                                                           \
-  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, ZM, KF, 0, kWaves>), dim3((unsigned)blocks), \
+  hipLaunchKernelGGL((gemm_kernel<BITS, WN_, GPT, ZM, KF, 0, kWaves, HALF>),                  \
+                     dim3((unsigned)blocks),                                                   \
                      dim3(64 * kWaves), 0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias, \
                      (_Float16*)y, M, N, K, group, group_magic(group), (int)tiles_m, tiles_n, \
                      (const _Float16*)e.res, e.ep)
@@ -404,10 +409,17 @@ int cu_count() {
 // times as many (2 x 13-16 KB stages: three blocks fit a CU, so the round model above does not
 // apply to them; tools/dev/gemm_bn.py, int4 g128 K = 4096): the GQA k / v projection N = 1024 at
 // M = 2048 53 -> 29 us; N = 4096 at M = 128-512 50 -> 24-32 us, M = 1024 57 -> 52 us.
+// Grids that small take 64-row blocks: 64 x 128 (three fit a CU) while that grid stays within
+// ~a round of blocks, 64 x 256 (two fit a CU, each B fragment feeding 4 MFMAs instead of 2) once
+// it would not (tools/dev/gemm_half.py: N = 4096 M = 768 / 1024 43.6 / 46.6 -> 40.7 / 43.0 us,
+// 4096 x 14336 M = 1024 146 -> 135 us, N = 6144 M = 512 42.6 -> 39.8 us, N = 28672 M = 128 42.7
+// -> 38.9 us; bit-identical); returned as kHalf256.
+constexpr int kHalf256 = 255;
 int pick_bn(int64_t M, int N, int bits) {
   if (bits == 8) return 256;
   const int64_t tm = (M + 127) / 128, cus = cu_count();
-  if (tm * ((N + 255) / 256) * 2 <= cus) return 128;
+  const int64_t n256 = (N + 255) / 256;
+  if (tm * n256 * 2 <= cus) return tm * n256 * 4 > cus ? kHalf256 : 128;
   static const int bn[3] = {256, 384, 512};
   static const double rel[3] = {1.0, 1.42, 1.84};
   int best = 256;
@@ -433,6 +445,8 @@ int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
       return launch_gemm_t<BITS, 384, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
     if (bn == 128)
       return launch_gemm_t<BITS, 128, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+    if (bn == kHalf256)
+      return launch_gemm_t<BITS, 256, GPT, ZM, true>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   }
   return launch_gemm_t<BITS, 256, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
 }
@@ -477,6 +491,7 @@ int gemm_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint1
 }
 }  // namespace
 
+// block columns pick_bn takes for this launch (255: the 64-row block of width 256)
 extern "C" int qlin_gemm_block_cols(int64_t M, int64_t N, int bits) {
   if (M < 1 || N < 1 || N > (1 << 30) || !(bits == 2 || bits == 3 || bits == 4 || bits == 8))
     return -QLIN_EINVAL;

@@ -222,9 +222,10 @@ def test_gptq_checkpoint_conversion(bits, group):
 
 def _pick_bn(M, N, cus):
     """Mirror of qlin_gemm.hip pick_bn (block width by rounds of blocks over the CUs; 128 = the
-    64 x 128 block for small grids)."""
-    if -(-M // 128) * -(-N // 256) * 2 <= cus:
-        return 128
+    64 x 128 block for small grids, 255 = the 64 x 256 block when that grid would exceed a round)."""
+    small = -(-M // 128) * -(-N // 256)
+    if small * 2 <= cus:
+        return 255 if small * 4 > cus else 128
     rel = {256: 1.0, 384: 1.42, 512: 1.84}
     best = None
     for bn in (256, 384, 512):
@@ -237,7 +238,7 @@ def _pick_bn(M, N, cus):
 
 
 @pytest.mark.parametrize("M,N,bn", [(4129, 6160, 512), (4129, 4112, 384), (8225, 4240, 256),
-                                    (333, 1040, 128), (65, 4112, 128)])
+                                    (333, 1040, 128), (65, 4112, 128), (1000, 4000, 255)])
 @pytest.mark.parametrize("bits,group", [(4, 128), (4, 64), (3, 64), (2, 32)])
 def test_gemm_block_widths(bits, group, M, N, bn):
     """The 128 x 256 / 384 / 512 and 64 x 128 block tiles (pick_bn: whole rounds of blocks over
@@ -266,7 +267,7 @@ def test_gemm_block_widths_bit_identical(bits, group):
     lib = qlin.load_library()
     K = 1024
     seen = set()
-    for N, Ms in ((4096, (2048, 8192)), (4112, (4129,))):
+    for N, Ms in ((4096, (1024, 2048, 8192)), (4112, (4129,))):
         qw, qsz, fl, _ = _packed(N, K, bits, group, seed=N + bits)
         xb = t(rand_x(max(Ms), K, seed=11))
         small = qlin.gemm(xb[:128].contiguous(), qw, qsz, None, N, K, bits, group, fl)
@@ -275,7 +276,7 @@ def test_gemm_block_widths_bit_identical(bits, group):
             seen.add(lib.qlin_gemm_block_cols(M, N, bits))
             big = qlin.gemm(xb[:M].contiguous(), qw, qsz, None, N, K, bits, group, fl)
             assert torch.equal(big[:128], small), f"M={M} N={N} b{bits} g{group}"
-    assert len(seen) >= 2, seen  # 256-CU MI355X: {256, 384, 512}
+    assert len(seen) >= 2, seen  # 256-CU MI355X: {255 (64 x 256), 256, 384, 512}
 
 
 @pytest.mark.parametrize("N", [8192 + 16 * 3 + 5, 8192 + 16])

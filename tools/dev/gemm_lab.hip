@@ -1,6 +1,20 @@
 // Development-only GEMM ablations: the product GEMM kernel with its ABL template bit set.
 #include "../../llama3-quantization_amd/csrc/qlin_gemm.hip"
 
+// 64-row blocks at width bn (256 / 384 / 512), 8 waves: two blocks per CU for one-round grids
+extern "C" int lab_gemm_half(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, uint16_t* y,
+                             int64_t M, int N, int K, int bn, void* stream) {
+  const int tn = (N + bn - 1) / bn, tm = (int)((M + 63) / 64);
+#define L(B) hipLaunchKernelGGL((gemm_kernel<4, B, 1, kZNarrow, true, 0, 8, true>), dim3(tm * tn), dim3(512), \
+                                0, (hipStream_t)stream, qw, qsz, (const _Float16*)x, nullptr,           \
+                                (_Float16*)y, M, N, K, 128, group_magic(128), tm, tn, nullptr, 0)
+  if (bn == 512) L(512);
+  else if (bn == 384) L(384);
+  else L(256);
+#undef L
+  return (int)hipGetLastError();
+}
+
 extern "C" int lab_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, uint16_t* y,
                         int64_t M, int N, int K, int abl, void* stream) {
   // abl bit 2: the wide (128 x 512) tile; bit 3: 8 waves per block (else 4)
