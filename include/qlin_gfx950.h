@@ -133,7 +133,11 @@ int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, in
  *   qlin_gemv_f16: matrix-core GEMV, 1 <= M <= 16 (decode / small batches).
  *   qlin_gemm_f16: MFMA (v_mfma_f32_*_f16) tiles, any M >= 1 (prefill / PPL windows).
  *   qlin_linear_f16: picks from M: GEMV for M <= 64 (16-row chunks), MFMA GEMM above.
- *   workspace: reserved, pass NULL.
+ *   workspace (qlin_gemm_f16): NULL, or at least qlin_linear_workspace_bytes(M, N, K, bits, group,
+ *     0) bytes of device memory (no alignment beyond 256 B, contents need not be initialised):
+ *     with it, launches whose grid of 64 x 128 blocks leaves most CUs idle split K over up to 8
+ *     block groups and reduce the fp32 partials in a second pass (fixed order: deterministic,
+ *     within fp32 rounding of the unsplit launch); without it they run unsplit.
  */
 int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                   const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
@@ -144,6 +148,11 @@ int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const
 int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                     const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
                     int group, void* stream);
+/* Workspace bytes qlin_gemm_f16 / qlin_linear_ep_f16 use for this launch (act_bits as passed to
+ * qlin_linear_ep_f16, 0 for qlin_gemm_f16): the act fake-quant x_dq region (when the quantizer
+ * kernel runs) followed by the split-K partials; 0 = none; -1 = invalid arguments. */
+int64_t qlin_linear_workspace_bytes(int64_t M, int64_t N, int64_t K, int bits, int group,
+                                    int act_bits);
 
 /*
  * Output columns per block that qlin_gemm_f16 picks for an M x N launch on the current device
@@ -170,6 +179,9 @@ int qlin_gemm_block_cols(int64_t M, int64_t N, int bits);
  * block recomputes the token's min / max; x 16-byte aligned, K % 8 == 0); otherwise the quantizer
  * kernel writes x_dq to `workspace` (fp16 [M, K], required then) before the GEMV / GEMM.
  * Same kernels and dispatch as qlin_linear_f16 (GEMV for M <= 64, MFMA GEMM above).
+ * workspace: NULL (only without the act quantizer kernel) or at least
+ * qlin_linear_workspace_bytes(M, N, K, bits, group, act_bits) bytes: the x_dq region, then the
+ * split-K partials of qlin_gemm_f16 (with too little the call writes past the buffer).
  */
 #define QLIN_EP_NONE     0
 #define QLIN_EP_RESIDUAL 1

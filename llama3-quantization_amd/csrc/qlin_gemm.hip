@@ -303,13 +303,17 @@ __device__ __forceinline__ void store_tile(const f4 (&acc)[MB][NB], int64_t M, i
 
 // ABL: development ablations (tools/dev/gemm_lab.hip): bit 0 skips the MFMA/dequant work, bit 1
 // the DMA after the first k-tile, bit 2 the dequant VALU; the library instantiates ABL = 0 only.
-// HALF: 64-row blocks (Cfg)
-template <int BITS, int WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4, bool HALF = false>
+// HALF: 64-row blocks (Cfg).  SPLIT: split-K — S blocks per output tile each run k-tiles
+// [s kts, (s + 1) kts) and write their fp32 accumulators, thread-linear, to `part`
+// ([tile][s][thread][MB NB 4]); gemm_splitk_reduce sums them in s order (deterministic) and
+// applies the epilogue
+template <int BITS, int WN_, int GPT, int ZM, bool KFULL, int ABL = 0, int NW = 4, bool HALF = false,
+          bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW) void gemm_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
     int64_t M, int N, int K, int group, uint32_t gmagic, int tiles_m, int tiles_n,
-    const _Float16* __restrict__ res, int ep) {
+    const _Float16* __restrict__ res, int ep, int S = 1, float* __restrict__ part = nullptr) {
   using C = Cfg<BITS, WN_, NW, HALF>;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * C::STAGE];
   GemmGeo g;
@@ -324,10 +328,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
   g.lane = threadIdx.x & 63;
   // XCD-aware order: dispatch puts block b on XCD b % 8; give each XCD a contiguous run of
   // (tile_m, tile_n) with n fastest so its blocks share x tiles in that XCD's L2
-  const int nblk = tiles_m * tiles_n;
+  const int nblk = tiles_m * tiles_n * (SPLIT ? S : 1);
   const int b = blockIdx.x;
   int lb = b;
   if ((nblk & 7) == 0) lb = (b & 7) * (nblk >> 3) + (b >> 3);
+  int split = 0;
+  if constexpr (SPLIT) {  // the S splits of a tile are adjacent: same XCD, shared x tile
+    split = lb % S;
+    lb /= S;
+  }
   const int tile_m = lb / tiles_n, tile_n = lb - tile_m * tiles_n;
   g.m0 = (int64_t)tile_m * C::BM;
   g.nt0 = (int64_t)tile_n * C::RT;
@@ -339,20 +348,68 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
 #pragma unroll
     for (int j = 0; j < C::NB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  load_stage<BITS, WN_, GPT, NW, HALF>(smem, g, 0, x, qw, qsz);
-  for (int kt = 0; kt < g.Kt; ++kt) {
+  int kt_beg = 0, kt_end = g.Kt;
+  if constexpr (SPLIT) {
+    const int kts = (g.Kt + S - 1) / S;
+    kt_beg = min(split * kts, g.Kt);
+    kt_end = min(kt_beg + kts, g.Kt);
+  }
+  if (kt_beg < kt_end) load_stage<BITS, WN_, GPT, NW, HALF>(smem, g, kt_beg, x, qw, qsz);
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
     // stage kt has landed for every wave, and every wave is done reading stage kt - 1
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
     __syncthreads();
-    if (!(ABL & 2) && kt + 1 < g.Kt)
-      load_stage<BITS, WN_, GPT, NW, HALF>(smem + ((kt + 1) & 1) * C::STAGE, g, kt + 1, x, qw, qsz);
+    if (!(ABL & 2) && kt + 1 < kt_end)
+      load_stage<BITS, WN_, GPT, NW, HALF>(smem + ((kt - kt_beg + 1) & 1) * C::STAGE, g, kt + 1, x,
+                                           qw, qsz);
     if (!(ABL & 1))
-      compute_stage<BITS, WN_, GPT, ZM, KFULL, NW, ABL, HALF>(smem + (kt & 1) * C::STAGE, g, kt, acc);
+      compute_stage<BITS, WN_, GPT, ZM, KFULL, NW, ABL, HALF>(smem + ((kt - kt_beg) & 1) * C::STAGE,
+                                                               g, kt, acc);
   }
 
+  if constexpr (SPLIT) {
+    f4* pp = reinterpret_cast<f4*>(part) +
+             (((int64_t)lb * S + split) * C::THREADS + threadIdx.x) * (C::MB * C::NB);
+#pragma unroll
+    for (int i = 0; i < C::MB; ++i)
+#pragma unroll
+      for (int j = 0; j < C::NB; ++j) pp[i * C::NB + j] = acc[i][j];
+    return;
+  }
   const int wm = g.wave / C::WGN, wn = g.wave % C::WGN;
   store_tile<C::MB, C::NB, C::BM>(acc, M, N, g.m0, g.m0 + wm * C::WM, g.nt0 + wn * C::NB, g.lane,
                                   bias, y, res, ep);
+}
+
+// split-K second pass: one block per output tile, each thread sums its S partial accumulators in
+// s order and stores them through the GEMM's own epilogue
+template <int BITS, int WN_, int NW>
+__global__ __launch_bounds__(64 * NW) void gemm_splitk_reduce(
+    const float* __restrict__ part, int S, int64_t M, int N, int tiles_n,
+    const _Float16* __restrict__ bias, _Float16* __restrict__ y,
+    const _Float16* __restrict__ res, int ep) {
+  using C = Cfg<BITS, WN_, NW>;
+  const int tile = blockIdx.x;
+  const int tile_m = tile / tiles_n, tile_n = tile - tile_m * tiles_n;
+  f4 acc[C::MB][C::NB];
+#pragma unroll
+  for (int i = 0; i < C::MB; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < S; ++sp) {
+    const f4* pp = reinterpret_cast<const f4*>(part) +
+                   (((int64_t)tile * S + sp) * C::THREADS + threadIdx.x) * (C::MB * C::NB);
+#pragma unroll
+    for (int i = 0; i < C::MB; ++i)
+#pragma unroll
+      for (int j = 0; j < C::NB; ++j) acc[i][j] += pp[i * C::NB + j];
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  const int64_t m0 = (int64_t)tile_m * C::BM;
+  const int64_t nt0 = (int64_t)tile_n * C::RT;
+  store_tile<C::MB, C::NB, C::BM>(acc, M, N, m0, m0 + wm * C::WM, nt0 + wn * C::NB, lane, bias, y,
+                                  res, ep);
 }
 
 uint32_t group_magic(int group) {
@@ -434,10 +491,36 @@ int pick_bn(int64_t M, int N, int bits) {
   return best;
 }
 
+// split-K launch of the 64 x 128 block (S splits, `part` = the caller's workspace)
+template <int BITS, int GPT, int ZM>
+int launch_gemm_split(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x,
+                      const uint16_t* bias, uint16_t* y, int64_t M, int N, int K, int group,
+                      hipStream_t st, const GemmEp& e, int S, float* part) {
+  using C = Cfg<BITS, 128, kWaves>;
+  const int tiles_n = (N + C::BN - 1) / C::BN;
+  const int tiles_m = (int)((M + C::BM - 1) / C::BM);
+  const int tiles = tiles_m * tiles_n;
+#define QLIN_GS(KF)                                                                            \
+  hipLaunchKernelGGL((gemm_kernel<BITS, 128, GPT, ZM, KF, 0, kWaves, false, true>),           \
+                     dim3((unsigned)(tiles * S)), dim3(64 * kWaves), 0, st, qw, qsz,           \
+                     (const _Float16*)x, nullptr, nullptr, M, N, K, group, group_magic(group), \
+                     tiles_m, tiles_n, nullptr, 0, S, part)
+  if (K % BK == 0) QLIN_GS(true);
+  else QLIN_GS(false);
+#undef QLIN_GS
+  hipLaunchKernelGGL((gemm_splitk_reduce<BITS, 128, kWaves>), dim3((unsigned)tiles),
+                     dim3(64 * kWaves), 0, st, part, S, M, N, tiles_n, (const _Float16*)bias,
+                     (_Float16*)y, (const _Float16*)e.res, e.ep);
+  return (int)hipGetLastError();
+}
+
 template <int BITS, int GPT, int ZM>
 int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
+                uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e,
+                int S = 1, float* part = nullptr) {
   if constexpr (BITS != 8) {
+    if (S > 1) return launch_gemm_split<BITS, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e,
+                                                       S, part);
     const int bn = pick_bn(M, N, BITS);
     if (bn == 512)
       return launch_gemm_t<BITS, 512, GPT, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
@@ -453,10 +536,30 @@ int launch_gemm(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
 
 template <int BITS, int ZM>
 int launch_gemm_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                  uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
-  if (group % 128 == 0) return launch_gemm<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
-  if (group % 64 == 0) return launch_gemm<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
-  return launch_gemm<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
+                  uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e,
+                  int S, float* part) {
+  if (group % 128 == 0)
+    return launch_gemm<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e, S, part);
+  if (group % 64 == 0)
+    return launch_gemm<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e, S, part);
+  return launch_gemm<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e, S, part);
+}
+
+// split-K parts for an M x N x K launch: grids of 64 x 128 blocks that leave most CUs idle (the
+// lone block is issue-bound at 24-50 us whatever M is) split K into up to 8 parts
+// of >= 4 k-tiles while the grid stays within one block per CU
+int splitk_parts(int64_t M, int64_t N, int64_t K, int bits) {
+  if (bits == 8 || M <= kSkinnyMaxM || pick_bn(M, (int)N, bits) != 128) return 1;
+  const int64_t tiles = ((M + 63) / 64) * ((N + 127) / 128), cus = cu_count();
+  const int64_t kt = (K + BK - 1) / BK;
+  int S = 1;
+  while (S < 8 && tiles * S * 2 <= cus && kt / (S * 2) >= 4) S *= 2;
+  return S;
+}
+int64_t splitk_bytes(int64_t M, int64_t N, int S) {
+  if (S <= 1) return 0;
+  const int64_t tiles = ((M + 63) / 64) * ((N + 127) / 128);
+  return tiles * S * (64 * kWaves) * 16 * 4;  // 64 x 128 block: MB NB 4 = 16 floats per thread
 }
 
 bool valid(int64_t M, int64_t N, int64_t K, int bits, int group) {
@@ -468,19 +571,24 @@ bool valid(int64_t M, int64_t N, int64_t K, int bits, int group) {
 }  // namespace
 
 namespace {
+// splitk_ws: the caller's split-K workspace (splitk_bytes of the launch) or nullptr (no split)
 int gemm_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
             const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
-            int64_t K, int bits, int group, int epilogue, void* stream) {
+            int64_t K, int bits, int group, int epilogue, void* stream, void* splitk_ws = nullptr) {
   if (!qweight || !qsz || !x || !y || !valid(M, N, K, bits, group)) return QLIN_EINVAL;
   if (M == 0 || N == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
   const GemmEp e{residual, epilogue};
   const int zm = zero_mode(flags);
   const int n = (int)N, k = (int)K;
+  const int S = splitk_ws ? splitk_parts(M, N, K, bits) : 1;
+  float* part = (float*)splitk_ws;
 #define QLIN_M(B)                                                                              \
-  return zm == kZFloat  ? launch_gemm_g<B, kZFloat>(qweight, qsz, x, bias, y, M, n, k, group, st, e) \
-         : zm == kZWide ? launch_gemm_g<B, kZWide>(qweight, qsz, x, bias, y, M, n, k, group, st, e)  \
-                        : launch_gemm_g<B, kZNarrow>(qweight, qsz, x, bias, y, M, n, k, group, st, e)
+  return zm == kZFloat                                                                         \
+             ? launch_gemm_g<B, kZFloat>(qweight, qsz, x, bias, y, M, n, k, group, st, e, S, part) \
+         : zm == kZWide                                                                        \
+             ? launch_gemm_g<B, kZWide>(qweight, qsz, x, bias, y, M, n, k, group, st, e, S, part)  \
+             : launch_gemm_g<B, kZNarrow>(qweight, qsz, x, bias, y, M, n, k, group, st, e, S, part)
   switch (bits) {
     case 2: QLIN_M(2);
     case 3: QLIN_M(3);
@@ -498,12 +606,27 @@ extern "C" int qlin_gemm_block_cols(int64_t M, int64_t N, int bits) {
   return pick_bn(M, (int)N, bits);
 }
 
+namespace {
+// act fake-quant x_dq region of qlin_linear_ep_f16's workspace (fp16 [M, K], 256-B aligned) when
+// that launch needs one, else 0
+int64_t act_ws_bytes(int64_t M, int64_t N, int64_t K, int act_bits) {
+  const bool fuse_act = M <= kSkinnyMaxM && N <= kActFuseMaxN;
+  return (act_bits && !fuse_act) ? (M * K * 2 + 255) / 256 * 256 : 0;
+}
+}  // namespace
+
+extern "C" int64_t qlin_linear_workspace_bytes(int64_t M, int64_t N, int64_t K, int bits,
+                                               int group, int act_bits) {
+  if (!valid(M < 1 ? 1 : M, N, K, bits, group) || M < 0 || act_bits < 0 || act_bits > 8) return -1;
+  return act_ws_bytes(M, N, K, act_bits) + splitk_bytes(M, N, splitk_parts(M, N, K, bits));
+}
+
 extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                              const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
                              int64_t N, int64_t K, int bits, int group, void* workspace,
                              void* stream) {
-  (void)workspace;
-  return gemm_ep(qweight, qsz, flags, x, bias, nullptr, y, M, N, K, bits, group, kEpNone, stream);
+  return gemm_ep(qweight, qsz, flags, x, bias, nullptr, y, M, N, K, bits, group, kEpNone, stream,
+                 workspace);
 }
 
 extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
@@ -540,6 +663,7 @@ extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, 
   // the quantizer launch + plain GEMV is cheaper (tools/dev/act_ab.py: 28672 x 4096 fused
   // 24.0 us vs 22.6 us; 4096 x 4096 fused 7.0 us vs 12.8 us)
   const bool fuse_act = act_bits && M <= kSkinnyMaxM && N <= kActFuseMaxN;
+  const int64_t act_bytes = act_ws_bytes(M, N, K, act_bits);
   if (act_bits && !fuse_act) {
     if (!workspace) return QLIN_EINVAL;
     const int rc = qlin_quantize(x, QLIN_F16, M, K, act_bits, (int)K,
@@ -560,5 +684,5 @@ extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, 
     return QLIN_OK;
   }
   return gemm_ep(qweight, qsz, flags, x, bias, residual, y, M, N, K, bits, group, epilogue,
-                 stream);
+                 stream, workspace ? (void*)((char*)workspace + act_bytes) : nullptr);
 }

@@ -47,6 +47,7 @@ SIGNATURES = {
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_block_cols": ([_l, _l, _i], _i),
+    "qlin_linear_workspace_bytes": ([_l, _l, _l, _i, _i, _i], _l),
     "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _i, _i, _p, _p],
                            _i),
     "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),
@@ -303,17 +304,21 @@ def _linear_call(fn_name, x, qweight, qsz, bias, N, K, bits, group, flags, extra
 
 def linear(x, qweight, qsz, bias, N, K, bits, group, flags=0):
     """Dispatching fused dequant-matmul (GEMV kernel for M <= 64 in 16-row chunks, MFMA GEMM
-    above)."""
-    return _linear_call("qlin_linear_f16", x, qweight, qsz, bias, N, K, bits, group, flags)
+    above, split-K for small grids): ``qlin_linear_ep_f16`` without an epilogue, which takes the
+    split-K workspace (``qlin_linear_f16``, the same dispatch without it, runs unsplit)."""
+    return linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags)
 
 
 def gemv(x, qweight, qsz, bias, N, K, bits, group, flags=0):
     return _linear_call("qlin_gemv_f16", x, qweight, qsz, bias, N, K, bits, group, flags)
 
 
-def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0):
+def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0, split=True):
+    """``qlin_gemm_f16``; ``split``: pass the split-K workspace (small grids split K)."""
+    M = x.numel() // K if K else 0
+    ws = _workspace(x.device, M, N, K, bits, group) if (split and M) else None
     return _linear_call("qlin_gemm_f16", x, qweight, qsz, bias, N, K, bits, group, flags,
-                        extra=(None,))
+                        extra=(_ptr(ws),))
 
 
 SKINNY_MAX_M = 64  # qlin_linear_*: M <= this runs the GEMV kernel
@@ -321,6 +326,15 @@ ACT_FUSE_MAX_N = 16384  # qlin_linear_ep_f16 fuses the act fake-quant into the G
 EP_NONE = 0
 EP_RESIDUAL = 1
 EP_SILU_MUL = 2
+
+
+def _workspace(device, M, N, K, bits, group, act_bits=0):
+    """The launch's workspace (qlin_linear_workspace_bytes: act fake-quant x_dq, split-K
+    partials) or None."""
+    nb = load_library().qlin_linear_workspace_bytes(M, N, K, bits, group, act_bits)
+    if nb < 0:
+        raise ValueError(f"invalid linear shape M={M} N={N} K={K} b{bits} g{group}")
+    return torch.empty(nb, dtype=torch.uint8, device=device) if nb else None
 
 
 def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NONE,
@@ -347,9 +361,7 @@ def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NON
     M = x.numel() // K if K else 0
     if M == 0:
         return y
-    ws = None
-    if act_bits and (M > SKINNY_MAX_M or N > ACT_FUSE_MAX_N):
-        ws = torch.empty(M, K, dtype=torch.float16, device=x.device)
+    ws = _workspace(x.device, M, N, K, bits, group, act_bits)
     rc = load_library().qlin_linear_ep_f16(_ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(bias),
                                            _ptr(residual), _ptr(y), M, N, K, bits, group,
                                            epilogue, act_bits, act_flags, _ptr(ws), _stream(x))

@@ -270,13 +270,43 @@ def test_gemm_block_widths_bit_identical(bits, group):
     for N, Ms in ((4096, (1024, 2048, 8192)), (4112, (4129,))):
         qw, qsz, fl, _ = _packed(N, K, bits, group, seed=N + bits)
         xb = t(rand_x(max(Ms), K, seed=11))
-        small = qlin.gemm(xb[:128].contiguous(), qw, qsz, None, N, K, bits, group, fl)
+        small = qlin.gemm(xb[:128].contiguous(), qw, qsz, None, N, K, bits, group, fl,
+                          split=False)
         assert lib.qlin_gemm_block_cols(128, N, bits) == 128
         for M in Ms:
             seen.add(lib.qlin_gemm_block_cols(M, N, bits))
-            big = qlin.gemm(xb[:M].contiguous(), qw, qsz, None, N, K, bits, group, fl)
+            big = qlin.gemm(xb[:M].contiguous(), qw, qsz, None, N, K, bits, group, fl,
+                            split=False)
             assert torch.equal(big[:128], small), f"M={M} N={N} b{bits} g{group}"
     assert len(seen) >= 2, seen  # 256-CU MI355X: {255 (64 x 256), 256, 384, 512}
+
+
+@pytest.mark.parametrize("M,N,K", [(65, 4096, 4096), (128, 4096, 14336), (200, 1040, 4096),
+                                   (256, 4096, 4096), (100, 512, 1024)])
+@pytest.mark.parametrize("bits,group", [(4, 128), (3, 64), (2, 32)])
+def test_gemm_split_k(M, N, K, bits, group):
+    """Small grids split K (qlin_linear_workspace_bytes > 0): the fp32 partials are reduced in a
+    fixed order — deterministic, within fp32 rounding of the unsplit launch, and every epilogue
+    (bias, residual, SiLU·mul) goes through the reduction pass."""
+    lib = qlin.load_library()
+    qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=M + N)
+    assert lib.qlin_linear_workspace_bytes(M, N, K, bits, group, 0) > 0
+    x = rand_x(M, K, seed=M)
+    bias = t((np.random.RandomState(3).randn(N) * 0.1).astype(np.float16))
+    y = qlin.gemm(t(x), qw, qsz, bias, N, K, bits, group, fl)
+    y2 = qlin.gemm(t(x), qw, qsz, bias, N, K, bits, group, fl)
+    assert torch.equal(y, y2)  # deterministic
+    ref = qlin.gemm(t(x), qw, qsz, bias, N, K, bits, group, fl, split=False)
+    assert (y.float() - ref.float()).abs().max().item() <= 2e-3 * ref.float().abs().max().item()
+    assert_close_to_ref(n(y), O.linear_ref(x, wdq, n(bias)), what=f"splitk M{M} N{N} K{K}")
+    r = t(rand_x(M, N, seed=5))
+    yr = qlin.linear_ep(t(x), qw, qsz, bias, N, K, bits, group, fl, epilogue=qlin.EP_RESIDUAL,
+                        residual=r)
+    assert (yr.float() - (r.float() + y.float())).abs().max().item() <= \
+        2e-3 * (r.float().abs().max().item() + y.float().abs().max().item())
+    if N % 16 == 0:
+        ys = qlin.linear_ep(t(x), qw, qsz, bias, N, K, bits, group, fl, epilogue=qlin.EP_SILU_MUL)
+        assert ys.shape == (M, N // 2) and torch.isfinite(ys).all()
 
 
 @pytest.mark.parametrize("N", [8192 + 16 * 3 + 5, 8192 + 16])
