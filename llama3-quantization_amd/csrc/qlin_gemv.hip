@@ -633,9 +633,12 @@ uint32_t group_magic(int group) {
 // >= 512 row tiles keep >= 4 tiles per wave (measured on the decode layer's shapes,
 // tools/dev/gemv_geo.py: 28,672 x 4,096 W = 8 12.6 us vs W = 4 13.3 us; 14,336 x 4,096 W = 8
 // 8.9 us vs W = 16 9.3 us; 4096 x 4096 and 6144 x 4096 keep W = 16)
+#ifndef GEMV_WAVE_TARGET  // dev sweep knob (tools/dev/Makefile libgv*.so)
+#define GEMV_WAVE_TARGET 8192
+#endif
 int pick_waves(int Nt, int Kt, int& tpw) {
   int W = 1;
-  while (W < kMaxWaves && (int64_t)Nt * W < 8192 && (Nt < 512 || Kt >= 8 * W)) W *= 2;
+  while (W < kMaxWaves && (int64_t)Nt * W < GEMV_WAVE_TARGET && (Nt < 512 || Kt >= 8 * W)) W *= 2;
   W = min(W, Kt);
   tpw = (Kt + W - 1) / W;
   return (Kt + tpw - 1) / tpw;
@@ -686,12 +689,14 @@ int launch_fast_t(const FastArgs& a, int Nt, int tpw, hipStream_t st) {
   if constexpr (MT == 1) {
     if (a.nw) {
       if (tpw <= 2) QLIN_GF(2, true);
-      else QLIN_GF(4, true);
+      else if (tpw <= 4) QLIN_GF(4, true);
+      else QLIN_GF(8, true);
       return (int)hipGetLastError();
     }
   }
   if (tpw <= 2) QLIN_GF(2, false);
-  else QLIN_GF(4, false);
+  else if (tpw <= 4) QLIN_GF(4, false);
+  else QLIN_GF(8, false);
 #undef QLIN_GF
   return (int)hipGetLastError();
 }
@@ -700,13 +705,16 @@ int launch_fast_t(const FastArgs& a, int Nt, int tpw, hipStream_t st) {
 // whose waves stream at most 4 tiles (tools/dev/fast_geo.py, M = 1: 4096 x 4096 W = 16 x 2 tiles
 // 4.30 -> 3.76 us, 6144 x 4096 5.48 -> 5.02, 28672 x 4096 W = 8 x 4 13.55 -> 12.67; the
 // LLaMA down projection 4096 x 14336, 7 tiles per wave, stays on gemv_kernel: 7.8 vs 8.3 us)
+#ifndef GEMV_FAST_MAX_TPW  // dev sweep knob: tiles per wave the fast path takes (4 or 8)
+#define GEMV_FAST_MAX_TPW 4
+#endif
 bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
   W = pick_waves(Nt, Kt, tpw);
   lw = 0;
   while ((2 << lw) <= W) ++lw;  // round W down to a power of two (W <= Kt)
   W = 1 << lw;
   tpw = (Kt + W - 1) / W;
-  return tpw <= 4;
+  return tpw <= GEMV_FAST_MAX_TPW;
 }
 
 template <int BITS, int MT, int ZM>
