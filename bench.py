@@ -2,10 +2,18 @@
 """Benchmark of the quantized-linear hot path on MI355X (BASELINE.json metric).
 
 Default workload (BASELINE.json configs[1]): LLaMA3-8B-shaped int4 group_size=128 dequant-GEMV at
-batch 1 — y[1, 4096] = x[1, 4096] @ W_dq[4096, 4096]^T through the fused gfx950 kernel, over a
+batch 1 — y[1, 4096] = x[1, 4096] @ W_dq[4096, 4096]^T through the fused gfx950 kernels, over a
 ring of R distinct synthetic matrices (W ~ N(0, 0.02^2), RTN int4 g128 by the build's own HIP
-quantizer; R >= 64 so 563 MB of codes cannot be served by the 256 MB Infinity Cache).
-One step = one pass over the ring (R launches, captured once in a HIP graph and replayed).
+quantizer; R >= 64 so 563 MB of codes cannot be served by the 256 MB Infinity Cache), each with
+its own activation row.  One step = one pass over the ring: R products.
+
+Two ways to run that step, both timed in every GEMV run (the headline `--mode`, the other under
+`other_mode`):
+  batched  (default) the whole ring as ONE strided-batch launch (qlin_gemv_batched_f16: the
+           streaming kernel, every output one MFMA chain in k order) — the kernel's HBM
+           throughput when the kernel boundary is paid once per ring;
+  launches one dependent qlin_gemv_f16 launch per matrix (graph-replayed) — the per-launch cost a
+           decode chain of dependent GEMVs pays (boundary + wave ramp of an 8.8 MB launch).
 
 Prints ONE JSON line (rank 0).  value = whole-job dequant-matmul TFLOP/s (sum over ranks: every
 rank streams its own ring, no collective in the data path -> weak scaling).
@@ -81,8 +89,15 @@ def parse():
                     help="strong scaling: every rank streams rows [r*N/P, (r+1)*N/P) of the SAME "
                          "ring (output-feature sharding, SURVEY.md §8(e)); default: weak scaling, "
                          "an independent ring per rank")
+    ap.add_argument("--mode", choices=("batched", "launches"), default="batched",
+                    help="GEMV workloads: 'batched' = the whole ring as one strided-batch launch "
+                         "(qlin_gemv_batched_f16); 'launches' = one dependent launch per matrix "
+                         "(the decode chain's per-launch cost); the other mode is timed too and "
+                         "reported beside it")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-mode", action="store_true",
+                    help="skip timing the other GEMV mode (batched / launches)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
 
@@ -175,43 +190,64 @@ def main():
         row0, N = 16 * t0, min(N_full, 16 * t1) - 16 * t0
     R = args.ring or ring
     gen = torch.Generator(device=dev)
-    mats = []
     zb = 2
+    hqq = args.workload.endswith("_hqq") or "_hqq_" in args.workload
+    # the ring lives in two stacked tensors (problem i = qw[i], qsz[i]): the strided batch reads
+    # it in one launch, the per-launch mode through views of the same bytes
+    qw_all = torch.zeros((R, *qlin.packed_shape(N, K, bits)), dtype=torch.int32, device=dev)
+    sz_all = torch.zeros((R, *qlin.sz_shape(N, K, group)), dtype=torch.int32, device=dev)
+    flags = set()
     for i in range(R):
         gen.manual_seed((0 if args.split else 1_000_003 * rank) + i)
         w = torch.empty(N_full, K, device=dev, dtype=torch.float16).normal_(0.0, 0.02, generator=gen)
         w = w[row0:row0 + N].contiguous()
         o = qlin.quantize(w, bits, group, 0, want_xdq=False, want_params=False, pack=True)
-        if args.workload.endswith("_hqq") or "_hqq_" in args.workload:
+        if hqq:
             # HQQ-style non-integral zero points: same codes and bytes, fp16 zero in the qsz word
             sc, zi = qlin.split_sz(o["qsz"], N)
             o["qsz"] = qlin.join_sz_float(sc, zi.to(torch.float16) + 0.375)
             o["flags"] = qlin.FLOAT_ZERO
-        mats.append((o["qweight"], o["qsz"], o["flags"]))
+        qw_all[i].copy_(o["qweight"])
+        sz_all[i].copy_(o["qsz"])
+        flags.add(o["flags"])
         del w, o
+    fl = qlin.FLOAT_ZERO if hqq else (qlin.WIDE_ZERO if qlin.WIDE_ZERO in flags else 0)
+    mats = [(qw_all[i], sz_all[i], fl) for i in range(R)]
     gen.manual_seed(1234)
-    x = torch.empty(M, K, device=dev, dtype=torch.float16).normal_(0.0, 1.0, generator=gen)
+    batched = kernel == "gemv" and args.mode == "batched"
+    # one activation row block per problem (the batch reads x[i]; the launches mode reads x[0])
+    xs = torch.empty(R, M, K, device=dev, dtype=torch.float16).normal_(0.0, 1.0, generator=gen)
+    x = xs[0]
     ys = [torch.empty(M, N, device=dev, dtype=torch.float16) for _ in range(min(R, 4))]
+    yb = torch.empty(R, M, N, device=dev, dtype=torch.float16)
     lib = qlin.load_library()
     fn = {"gemv": lib.qlin_gemv_f16, "linear": lib.qlin_linear_f16,
           "gemm": lib.qlin_gemm_f16}[kernel]
 
-    def step():
+    def step_launches():
         st = torch.cuda.current_stream(dev).cuda_stream
-        for i, (qw, qsz, fl) in enumerate(mats):
+        for i, (qw, qsz, fl_) in enumerate(mats):
             y = ys[i % len(ys)]
             if kernel in ("gemv", "linear"):
-                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl, x.data_ptr(), None,
+                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl_, x.data_ptr(), None,
                         y.data_ptr(), M, N, K, bits, group, st)
             else:
-                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl, x.data_ptr(), None, y.data_ptr(),
+                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl_, x.data_ptr(), None, y.data_ptr(),
                         M, N, K, bits, group, None, st)
             if rc != 0:
                 raise RuntimeError(f"kernel failed: {rc}")
 
+    def step_batched():
+        st = torch.cuda.current_stream(dev).cuda_stream
+        rc = lib.qlin_gemv_batched_f16(qw_all.data_ptr(), qw_all[0].numel(), sz_all.data_ptr(),
+                                       sz_all[0].numel(), fl, xs.data_ptr(), M * K, None, 0,
+                                       yb.data_ptr(), M * N, R, M, N, K, bits, group, st)
+        if rc != 0:
+            raise RuntimeError(f"kernel failed: {rc}")
+
     use_graph = not args.no_graph and kernel in ("gemv", "linear")
 
-    def make_runner():
+    def make_runner(step):
         if not use_graph:
             return step
         s = torch.cuda.Stream(dev)
@@ -224,59 +260,84 @@ def main():
             step()
         return graph.replay
 
-    run = make_runner()
+    def timed(run, steps, warmup):
+        """HIP events on the launch stream around `steps` runs; barrier + synchronize on both
+        sides; MAX over ranks."""
+        for _ in range(warmup):
+            run()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(steps):
+            run()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        wall_ = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t = torch.tensor([e0.elapsed_time(e1) / 1e3], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), wall_
 
-    for _ in range(args.warmup):
-        run()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record()
-    for _ in range(args.steps):
-        run()
-    e1.record()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev_s = e0.elapsed_time(e1) / 1e3
-    t = torch.tensor([ev_s], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed, wall = timed(make_runner(step_batched if batched else step_launches), args.steps,
+                          args.warmup)
 
-    launches = args.steps * R
     flops = 2.0 * M * N * K
     nbytes = algo_bytes(M, N, K, bits, group)
     read_bytes = algo_bytes(M, N, K, bits, group, zb)
-    per_launch_s = elapsed / launches
+    products = args.steps * R  # (1 x M) x (N x K) products in the timed region
+    kernel_launches = args.steps * (1 if batched else R)
+    per_product_s = elapsed / products
     # whole job: weak = every rank's full ring; strong = the one shared ring (rows summed)
     job_flops = 2.0 * M * N_full * K if args.split else flops * world
-    value = job_flops * launches / elapsed / 1e12
+    value = job_flops * products / elapsed / 1e12
     hbm_bound = kernel in ("gemv", "linear") or M <= 256
-    if hbm_bound:
-        roof = {"bound": "hbm", "achieved": round(nbytes / per_launch_s / 1e9, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+
+    def roofline(per_product, launch_products):
+        if hbm_bound:
+            r = {"bound": "hbm", "achieved": round(nbytes / per_product / 1e9, 1),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+        else:
+            r = {"bound": "mfma", "achieved": round(flops / per_product / 1e12, 2),
+                 "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s"}
+        r["frac"] = round(r["achieved"] / r["peak"], 4)
+        r["traffic"] = None
+        pmc_name = args.workload + ("_batched" if launch_products > 1 else "")
+        pmc = _pmc_traffic(pmc_name) if not (args.split and world > 1) else None
+        if pmc is not None:
+            r["traffic"] = round(pmc["fetch_bytes_per_launch"])
+            r["traffic_source"] = pmc["file"]
+        r["bytes_per_launch"] = nbytes * launch_products
+        r["bytes_read_per_launch"] = read_bytes * launch_products
+        r["us_per_launch"] = round(per_product * launch_products * 1e6, 3)
+        r["products_per_launch"] = launch_products
+        return r
+
+    roof = roofline(per_product_s, R if batched else 1)
+    if batched:
+        roof["timing"] = ("HIP events over the timed region / launches (one strided-batch launch "
+                          f"of {R} GEMVs per step, graph-replayed)")
     else:
-        roof = {"bound": "mfma", "achieved": round(flops / per_launch_s / 1e12, 2),
-                "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s"}
-    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-    roof["traffic"] = None
-    pmc = _pmc_traffic(args.workload) if not (args.split and world > 1) else None
-    if pmc is not None:
-        roof["traffic"] = round(pmc["fetch_bytes_per_launch"])
-        roof["traffic_source"] = pmc["file"]
-    roof["bytes_per_launch"] = nbytes
-    roof["bytes_read_per_launch"] = read_bytes
-    roof["us_per_launch"] = round(per_launch_s * 1e6, 3)
-    roof["timing"] = ("HIP events over the timed region / launches (graph replay of the ring; "
-                      "includes the inter-kernel dispatch gap)" if use_graph else
-                      "HIP events over the timed region / launches (eager)")
+        roof["timing"] = ("HIP events over the timed region / launches (graph replay of the ring; "
+                          "includes the inter-kernel dispatch gap)" if use_graph else
+                          "HIP events over the timed region / launches (eager)")
+    other = None
+    if kernel == "gemv" and not args.no_other_mode:
+        # the other mode, timed the same way, reported beside the headline
+        o_el, _ = timed(make_runner(step_launches if batched else step_batched),
+                        max(5, args.steps // 2), max(2, args.warmup // 2))
+        o_per = o_el / (max(5, args.steps // 2) * R)
+        other = roofline(o_per, 1 if batched else R)
+        other["mode"] = "launches" if batched else "batched"
+        other["value"] = round(job_flops / o_per / 1e12, 4)
 
     out = {
         "metric": "dequant-matmul TFLOP/s + HBM GB/s, int4 g128 4096x4096; LLaMA3-8B PPL delta",
@@ -286,20 +347,24 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "kernel_launches_per_step": kernel_launches // args.steps,
         "higher_is_better": True,
         "scaling": "strong" if args.split else "weak",
         "vs_baseline": None,
         "dtype": "f16",
         "data": "synthetic",
-        "hbm_GBps_total": round(nbytes * launches * world / elapsed / 1e9, 1),
+        "hbm_GBps_total": round(nbytes * products * world / elapsed / 1e9, 1),
         "config": {"workload": args.workload, "note": note, "M": M, "N": N_full, "K": K,
                    "N_per_rank": N, "bits": bits, "group_size": group, "ring": R,
                    "sz_bytes_per_group": 2 + zb, "graph": use_graph,
+                   "mode": ("batched" if batched else "launches") if kernel == "gemv" else kernel,
                    "parallelism": (f"strong x{world} (output rows split, no collective)"
                                    if args.split else f"weak x{world} (independent rings)")},
         "roofline": roof,
         "wall_s": round(wall, 4),
     }
+    if other is not None:
+        out["other_mode"] = other
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(M, N, K, bits, group, args.cpu_seconds) \
             if kernel != "gemm" else cpu_baseline(min(M, 32), N, K, bits, group, args.cpu_seconds)

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 4
+#define QLIN_ABI_VERSION 5
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -145,6 +145,26 @@ int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const
 int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                   const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
                   int group, void* workspace, void* stream);
+/*
+ * Strided batch of independent decode products in one launch:
+ *   y[b] = x[b] @ W_dq[b]^T (+ bias[b]),  b < batch (<= 65535), 1 <= M <= 16,
+ * problem b's operands at qweight + b*qweight_stride, qsz + b*qsz_stride (uint32 words),
+ * x + b*x_stride, bias + b*bias_stride, y + b*y_stride (fp16 elements); every problem has the
+ * same M, N, K, bits, group and flags.
+ * The same QuantLinear.forward F.linear (quant/int_linear.py:62) as qlin_gemv_f16, applied to
+ * several independent QuantLinear modules of one shape at once (e.g. one decode step over the
+ * modules of a ring of layers' weights); one kernel boundary per batch instead of per matrix.
+ * x_stride / bias_stride may be 0 (one activation / bias shared by every problem); other strides
+ * smaller than one problem's extent return QLIN_EINVAL.  M <= 4 with K % 512 == 0 and group a
+ * multiple of 128 (or 32 / 64) runs the streaming kernel: each output is one MFMA chain in k
+ * order, bit-identical to qlin_gemm_f16 without workspace; other shapes run one qlin_gemv_f16
+ * launch per problem.
+ */
+int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_stride, const uint32_t* qsz,
+                          int64_t qsz_stride, int flags, const uint16_t* x, int64_t x_stride,
+                          const uint16_t* bias, int64_t bias_stride, uint16_t* y,
+                          int64_t y_stride, int64_t batch, int64_t M, int64_t N, int64_t K,
+                          int bits, int group, void* stream);
 int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                     const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
                     int group, void* stream);

@@ -28,6 +28,7 @@
 // tiles each, PF = 2 or 4 tiles in flight per wave) and combine their 16 x M partials through
 // LDS.  Design measurements: tools/dev/gemv_lab.hip, DESIGN.md §4.
 #include "qlin_common.h"
+#include "qlin_gemv_tile.h"
 #include "../../include/qlin_gfx950.h"
 
 #include <type_traits>
@@ -51,19 +52,6 @@ struct Ep {  // output epilogue (qlin_common.h kEp*) and fused activation fake-q
   const uint16_t* res;
   int ep;
   ActQ aq;
-};
-constexpr int kGemvMaxM = 16;  // one MFMA row block
-
-template <int BITS, int GPT>
-struct WTile {
-  Piece<BITS> pc;
-  uint32_t sz[GPT];  // packed (scale, zero) of each group slot, decoded only at use
-};
-
-// raw x words of one tile for MT rows: lane l holds 2*MT halfs of row l / (64/MT)
-template <int MT>
-struct XRaw {
-  uint32_t w[MT];
 };
 
 struct Geo {
@@ -133,25 +121,6 @@ __device__ __forceinline__ void fake_quant_x(XRaw<MT>& r, const ActQ& aq, float 
     const float hi = fq<_Float16>((float)v.y, sc, zp, has_zp, P, xi);
     r.w[i] = as_u32(h2{(_Float16)lo, (_Float16)hi});
   }
-}
-
-template <int MT>
-__device__ __forceinline__ void park_x(h8 (&xa)[4], const XRaw<MT>& r, uint32_t* slot, int lane,
-                                       int n_in) {
-  if constexpr (MT == 1) {
-    slot[lane] = r.w[0];
-  } else if constexpr (MT == 2) {
-    *reinterpret_cast<uint2*>(slot + 2 * lane) = make_uint2(r.w[0], r.w[1]);
-  } else {
-#pragma unroll
-    for (int c = 0; c < MT / 4; ++c)
-      reinterpret_cast<uint4*>(slot + MT * lane)[c] =
-          make_uint4(r.w[4 * c], r.w[4 * c + 1], r.w[4 * c + 2], r.w[4 * c + 3]);
-  }
-  const int m = min(n_in, MT - 1);
-  const uint4* b = reinterpret_cast<const uint4*>(slot + 64 * m) + (lane >> 4);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, b[4 * s]);
 }
 
 // NTB row tiles per block share each parked x tile (x is re-read from L2 once per block, so
@@ -418,10 +387,13 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
   const int nt = blockIdx.x;
+  const _Float16* ax = a.x;
+  const _Float16* abias = a.bias;
+  _Float16* ay = a.y;
   const uint32_t* qw = a.qw + (int64_t)nt * a.Kt * (64 * BITS) + lane * BITS;
   const uint32_t* sz = a.qsz + (int64_t)nt * a.G * kTileN + n_in;
   constexpr int LPR = 64 / MT;  // lanes per x row
-  const _Float16* xr = a.x + (int64_t)min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
+  const _Float16* xr = ax + (int64_t)min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
   const int nts = (a.Kt - wave + a.W - 1) >> a.lw;  // >= 1: W <= Kt
   const int ktl = wave + ((nts - 1) << a.lw);        // the wave's last tile
 
@@ -486,9 +458,9 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   const int om = min(tid / (NO / MT), a.M - 1), on = tid % (NO / MT);  // output (row m, column n)
   const int64_t orow = (int64_t)nt * kTileN + on;
   const bool oval = tid < NO && tid / (NO / MT) < a.M && orow + (EP == kEpSiluMul ? 8 : 0) < a.N;
-  const _Float16* bsrc = a.bias ? a.bias + min(orow, (int64_t)a.N - 1) : a.x;
+  const _Float16* bsrc = abias ? abias + min(orow, (int64_t)a.N - 1) : ax;
   const _Float16 ob0 = bsrc[0];
-  const _Float16 ob1 = EP == kEpSiluMul ? bsrc[a.bias ? 8 : 0] : ob0;
+  const _Float16 ob1 = EP == kEpSiluMul ? bsrc[abias ? 8 : 0] : ob0;
   _Float16 ores = 0;
   if constexpr (EP == kEpResidual) ores = a.res[(int64_t)om * a.N + min(orow, (int64_t)a.N - 1)];
 
@@ -570,17 +542,17 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
     const f4 p = r[0], q = r[1], c = r[2], d = r[3];
     const f4 e = (p + q) + (c + d);
     float t = (e[0] + e[1]) + (e[2] + e[3]);
-    if (a.bias) t += (float)b;
+    if (abias) t += (float)b;
     return (float)(_Float16)t;  // F.linear's fp16 output
   };
   if (oval) {  // wave 0 only (tid < NO <= 64)
     if constexpr (EP == kEpSiluMul) {  // 8 outputs per tile and row
       const float g = total(om * kTileN + on, ob0), u = total(om * kTileN + on + 8, ob1);
-      a.y[(int64_t)om * (a.N >> 1) + nt * 8 + on] = (_Float16)(silu_rn16(g) * u);
+      ay[(int64_t)om * (a.N >> 1) + nt * 8 + on] = (_Float16)(silu_rn16(g) * u);
     } else {
       float t = total(om * kTileN + on, ob0);
       if constexpr (EP == kEpResidual) t += (float)ores;
-      a.y[(int64_t)om * a.N + orow] = (_Float16)t;
+      ay[(int64_t)om * a.N + orow] = (_Float16)t;
     }
   }
 }
@@ -617,11 +589,6 @@ __global__ __launch_bounds__(256) void dequant_kernel(
   one(std::integral_constant<int, 1>{});
   one(std::integral_constant<int, 2>{});
   one(std::integral_constant<int, 3>{});
-}
-
-bool valid_layout(int64_t N, int64_t K, int bits, int group) {
-  return N >= 0 && N <= (1 << 30) && K > 0 && K % 32 == 0 && K <= (1 << 20) && group > 0 &&
-         group % 32 == 0 && K % group == 0 && (bits == 2 || bits == 3 || bits == 4 || bits == 8);
 }
 
 uint32_t group_magic(int group) {

@@ -1,0 +1,291 @@
+// qlin_gemv_batched.hip — strided batch of independent decode GEMVs in one launch (gfx950).
+//
+// qlin_gemv_batched_f16: y[b] = x[b] @ W_dq[b]^T (+ bias[b]) for b < batch, the same
+// QuantLinear.forward -> F.linear(input, W_dq, bias) (quant/int_linear.py:62) as qlin_gemv_f16,
+// for many same-shaped packed matrices at once.  The single-launch GEMV is latency-bound (a
+// dependent 4096^2 launch pays a ~1.5 us kernel boundary and a ~1 us wave ramp for 8.8 MB,
+// DESIGN.md §4); a batch pays them once and is bound by HBM bandwidth instead.
+#include "qlin_common.h"
+#include "qlin_gemv_tile.h"
+
+#include <algorithm>
+#include <atomic>
+#include <type_traits>
+
+using namespace qlin;
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Batched streaming GEMV: a launch over a batch is throughput-, not latency-bound, so the
+// decomposition differs from the single-launch fast path (qlin_gemv.hip):
+//   - ONE wave owns whole 16-row tile rows and streams all of their K (int4, K = 4096: a
+//     contiguous 32 KB region per tile row) with PF tiles in flight, accumulating each tile row in
+//     a single MFMA chain in k order: no cross-wave reduction, no LDS barrier, no block phases (a
+//     block is 4 independent waves).  Each output is one v_mfma_f32_16x16x32_f16 chain over
+//     k = 0, 32, 64, ... -- the order of qlin_gemm_f16 (bit-identical to it without split-K);
+//   - the grid is sized to the resident capacity (CUs x blocks per CU from the occupancy query)
+//     and wave w takes the contiguous tile rows [w T / Wt, (w + 1) T / Wt) of the batch's T, so
+//     every wave streams from start to end (one-tile-row-per-wave grids ran in ~2.3 rounds and the
+//     last, partial round streamed with a third of the chip's loads in flight);
+//   - the prefetch runs across tile-row boundaries (rounds of PF tiles never straddle one:
+//     Kt % PF == 0), so a wave's loads never drain between its rows;
+//   - blocks are remapped so that each XCD takes a contiguous run of tile rows (a problem's x stays
+//     in one L2).
+// ---------------------------------------------------------------------------------------------
+struct StreamArgs {
+  const uint32_t* qw;
+  const uint32_t* qsz;
+  const _Float16* x;
+  const _Float16* bias;
+  _Float16* y;
+  int64_t bs_qw, bs_sz, bs_x, bs_b, bs_y;  // per-problem element strides
+  int M, N, K, Kt, G, Nt;
+  int64_t T;         // tile rows over the batch (batch x Nt)
+  int64_t Wt;        // waves of the launch (<= T); wave w streams tile rows [wT/Wt, (w+1)T/Wt)
+  uint32_t cmagic;   // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
+  int xcd_chunk;     // > 0: blocks per XCD of the remapped order (grid % 8 == 0)
+};
+
+constexpr int kStreamWaves = 4;
+#ifndef GEMV_STREAM_PF  // tiles in flight per wave (dev knob)
+#define GEMV_STREAM_PF 8
+#endif
+#ifndef GEMV_STREAM_PERSIST  // dev A/B knob: 0 = one tile row per wave (grid of T waves)
+#define GEMV_STREAM_PERSIST 1
+#endif
+
+template <int BITS, int MT, int GPT, int ZM, int PF>
+__global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const StreamArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t xs[kStreamWaves][64 * MT];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, n_in = lane & 15;
+  int blk = blockIdx.x;
+  if (a.xcd_chunk > 0) blk = (blk & 7) * a.xcd_chunk + (blk >> 3);  // XCD j: a contiguous run
+  const int64_t w = (int64_t)blk * kStreamWaves + wave;
+  if (w >= a.Wt) return;  // wave-uniform; no barriers below
+  const int64_t r0 = w * a.T / a.Wt, r1 = (w + 1) * a.T / a.Wt;
+  if (r0 >= r1) return;
+  constexpr int LPR = 64 / MT;
+  const int xlane = min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
+
+  // load stream: tile row lr, round start lkt, its operand bases
+  int64_t lr = r0;
+  int lkt = 0;
+  const uint32_t* lqw;
+  const uint32_t* lsz;
+  const _Float16* lx;
+  auto set_row = [&](int64_t r) {
+    const int64_t b = r / a.Nt;
+    const int nt = (int)(r - b * a.Nt);
+    lqw = a.qw + b * a.bs_qw + (int64_t)nt * a.Kt * (64 * BITS) + lane * BITS;
+    lsz = a.qsz + b * a.bs_sz + (int64_t)nt * a.G * kTileN + n_in;
+    lx = a.x + b * a.bs_x + xlane;
+  };
+  set_row(lr);
+  auto group_of_tile = [&](int kt) {
+    return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
+  };
+  WTile<BITS, GPT> wt[PF];
+  XRaw<MT> xq[PF];
+  auto load = [&](int u, int kt) {
+    wt[u].pc = load_piece_nt<BITS>(lqw + kt * (64 * BITS));
+    const int g0 = group_of_tile(kt);
+#pragma unroll
+    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = lsz[(g0 + s) * kTileN];
+    const _Float16* p = lx + kt * kTileK;
+    if constexpr (MT == 1) {
+      xq[u].w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (MT == 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      xq[u].w[0] = v.x; xq[u].w[1] = v.y;
+    } else {
+      const uint4 v = *reinterpret_cast<const uint4*>(p);
+      xq[u].w[0] = v.x; xq[u].w[1] = v.y; xq[u].w[2] = v.z; xq[u].w[3] = v.w;
+    }
+  };
+  const Magics mg = make_magics<BITS>();
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  uint32_t* slot = &xs[wave][0];
+  auto tile = [&](int u) {
+    h8 xa[4];
+    park_x<MT>(xa, xq[u], slot, lane, n_in);
+    auto step = [&](auto S_) {
+      constexpr int S = decltype(S_)::value;
+      uint32_t v[4];
+      const GroupQ gq = make_group_w<BITS, ZM>(wt[u].sz[S * GPT / 4]);
+      dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
+      const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+  };
+  // C row m = 4q + e sits in lane n + 16q, element e: lanes 0..15 hold rows 0..3
+  auto store = [&](int64_t r) {
+    const int64_t b = r / a.Nt;
+    const int64_t row = (r - b * a.Nt) * kTileN + n_in;
+    if (lane < 16 && row < a.N) {
+      const float bv = a.bias ? (float)a.bias[b * a.bs_b + row] : 0.f;
+#pragma unroll
+      for (int e = 0; e < MT && e < 4; ++e) {
+        if (e < a.M) {
+          float t = acc[e];
+          if (a.bias) t += bv;
+          a.y[b * a.bs_y + (int64_t)e * a.N + row] = (_Float16)t;
+        }
+      }
+    }
+    acc = f4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // rounds of PF tiles (Kt % PF == 0: a round never straddles two tile rows); every round but
+  // the last refills each slot right after computing it with the next round's tile
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load(u, u);
+  int64_t cr = r0;  // compute stream: tile row, round start
+  int ckt = 0;
+  const int64_t rounds = (r1 - r0) * (a.Kt / PF);
+  for (int64_t q = 0; q + 1 < rounds; ++q) {
+    lkt += PF;
+    if (lkt == a.Kt) {  // wave-uniform
+      lkt = 0;
+      set_row(++lr);
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      tile(u);
+      load(u, lkt + u);
+    }
+    ckt += PF;
+    if (ckt == a.Kt) {  // wave-uniform: the tile row is complete
+      store(cr);
+      ckt = 0;
+      ++cr;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u) tile(u);
+  store(cr);
+}
+
+// resident blocks of a stream-kernel instance per CU (occupancy query, cached per instance)
+template <typename Kern>
+int blocks_per_cu(Kern k) {
+  static const int nb = [&] {
+    int n = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * kStreamWaves, 0) ==
+                       hipSuccess && n > 0
+               ? n : 1;
+  }();
+  return nb;
+}
+
+// CUs of the current device, cached per device id
+int stream_cu_count() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  int n = dev < kMaxDev ? cache[dev].load(std::memory_order_relaxed) : 0;
+  if (n > 0) return n;
+  int c = 0;
+  n = (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+       c > 0) ? c : 256;
+  if (dev < kMaxDev) cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+template <int BITS, int MT, int GPT, int ZM, int PF>
+int launch_stream_pf(StreamArgs a, hipStream_t st) {
+  auto k = gemv_stream_kernel<BITS, MT, GPT, ZM, PF>;
+  int64_t Wt = a.T;
+  if (GEMV_STREAM_PERSIST)
+    Wt = std::min<int64_t>(a.T, (int64_t)stream_cu_count() * blocks_per_cu(k) * kStreamWaves);
+  a.Wt = Wt;
+  const int64_t blocks = (Wt + kStreamWaves - 1) / kStreamWaves;
+  a.xcd_chunk = blocks % 8 == 0 ? (int)(blocks / 8) : 0;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * kStreamWaves), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int BITS, int MT, int GPT, int ZM>
+int launch_stream_t(const StreamArgs& a, hipStream_t st) {
+  if (a.Kt % GEMV_STREAM_PF == 0) return launch_stream_pf<BITS, MT, GPT, ZM, GEMV_STREAM_PF>(a, st);
+  return launch_stream_pf<BITS, MT, GPT, ZM, 4>(a, st);  // Kt % 4 == 0 (host)
+}
+
+}  // namespace
+
+// Strided batch of independent products y_b = x_b @ W_dq,b^T (+ bias_b), b < batch, in ONE launch
+// (grid Nt x batch): the per-launch floor of a dependent 4096^2 GEMV (kernel boundary + wave ramp,
+// DESIGN.md §4) is paid once per batch instead of once per matrix.  Problems the decode fast path
+// does not take (M > 4, K % 128, tiles per wave > 4) run as one gemv launch each.
+extern "C" int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_stride,
+                                     const uint32_t* qsz, int64_t qsz_stride, int flags,
+                                     const uint16_t* x, int64_t x_stride, const uint16_t* bias,
+                                     int64_t bias_stride, uint16_t* y, int64_t y_stride,
+                                     int64_t batch, int64_t M, int64_t N, int64_t K, int bits,
+                                     int group, void* stream) {
+  if (!qweight || !qsz || !x || !y || batch < 0 || batch > 65535 || M < 1 || M > kGemvMaxM ||
+      !valid_layout(N, K, bits, group))
+    return QLIN_EINVAL;
+  const int64_t Nt = (N + kTileN - 1) / kTileN, Kt = (K + kTileK - 1) / kTileK;
+  // strides must not let two problems' packed operands or outputs overlap; x and bias may be
+  // shared (stride 0: several matrices applied to one activation)
+  if (qweight_stride < Nt * Kt * 64 * bits || qsz_stride < Nt * (K / group) * kTileN ||
+      (x_stride != 0 && x_stride < M * K) || y_stride < M * N ||
+      (bias && bias_stride != 0 && bias_stride < N))
+    return QLIN_EINVAL;
+  if (batch == 0 || N == 0) return QLIN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  // the streaming kernel: M <= 4, whole tiles (a multiple of 4 per row), group a multiple of 128
+  // or 32 / 64
+  if (M <= 4 && K % kTileK == 0 && (group % kTileK == 0 || group == 32 || group == 64) &&
+      Kt % 4 == 0) {
+    StreamArgs a;
+    a.qw = qweight; a.qsz = qsz; a.x = (const _Float16*)x; a.bias = (const _Float16*)bias;
+    a.y = (_Float16*)y;
+    a.bs_qw = qweight_stride; a.bs_sz = qsz_stride; a.bs_x = x_stride;
+    a.bs_b = bias ? bias_stride : 0; a.bs_y = y_stride;
+    a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Kt = (int)(K / kTileK); a.G = (int)(K / group);
+    a.Nt = (int)Nt;
+    a.T = Nt * batch;
+    const uint64_t c = group % kTileK == 0 ? (uint64_t)(group / kTileK) : 1;
+    a.cmagic = (uint32_t)(((1ull << 31) + c - 1) / c);
+    const int zm = zero_mode(flags), m = (int)M;
+#define QLIN_SM(B, Z, G)                                                                       \
+  return m == 1 ? launch_stream_t<B, 1, G, Z>(a, st)                                   \
+         : m == 2 ? launch_stream_t<B, 2, G, Z>(a, st)                                 \
+                  : launch_stream_t<B, 4, G, Z>(a, st)
+#define QLIN_SG(B, Z)                                                                          \
+  if (group % kTileK == 0) QLIN_SM(B, Z, 1);                                                   \
+  if (group == 64) QLIN_SM(B, Z, 2);                                                           \
+  QLIN_SM(B, Z, 4)
+#define QLIN_SB(B)                                                                             \
+  if (zm == kZFloat) { QLIN_SG(B, kZFloat); }                                                  \
+  if (zm == kZWide) { QLIN_SG(B, kZWide); }                                                    \
+  QLIN_SG(B, kZNarrow)
+    switch (bits) {
+      case 2: QLIN_SB(2);
+      case 3: QLIN_SB(3);
+      case 4: QLIN_SB(4);
+      default: QLIN_SB(8);
+    }
+#undef QLIN_SB
+#undef QLIN_SG
+#undef QLIN_SM
+  }
+  // anything else: one launch per problem
+  for (int64_t b = 0; b < batch; ++b) {
+    const int rc = qlin::gemv_ep(qweight + b * qweight_stride, qsz + b * qsz_stride, flags,
+                                 x + b * x_stride, bias ? bias + b * bias_stride : nullptr,
+                                 nullptr, y + b * y_stride, M, N, K, bits, group, kEpNone, 0, 0,
+                                 stream);
+    if (rc) return rc;
+  }
+  return QLIN_OK;
+}

@@ -16,7 +16,7 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -45,6 +45,8 @@ SIGNATURES = {
     "qlin_dequant_f16": ([_p, _p, _i, _l, _l, _i, _i, _p, _p], _i),
     "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
+    "qlin_gemv_batched_f16": ([_p, _l, _p, _l, _i, _p, _l, _p, _l, _p, _l, _l, _l, _l, _l, _i, _i,
+                               _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_block_cols": ([_l, _l, _i], _i),
     "qlin_linear_workspace_bytes": ([_l, _l, _l, _i, _i, _i], _l),
@@ -311,6 +313,41 @@ def linear(x, qweight, qsz, bias, N, K, bits, group, flags=0):
 
 def gemv(x, qweight, qsz, bias, N, K, bits, group, flags=0):
     return _linear_call("qlin_gemv_f16", x, qweight, qsz, bias, N, K, bits, group, flags)
+
+
+def gemv_batched(x, qweight, qsz, bias, N, K, bits, group, flags=0, out=None):
+    """``qlin_gemv_batched_f16``: B independent decode products in one launch.
+
+    x [B, M, K] fp16 (M <= 16), or [M, K] shared by every problem; qweight [B, *packed_shape],
+    qsz [B, *sz_shape] (one packed matrix per problem, same N / K / bits / group / flags); bias
+    [B, N] or None.  Returns y [B, M, N]: for M <= 4 and K % 512 == 0 each y[b] is bit-identical
+    to ``gemm(x[b], ..., split=False)`` (one MFMA chain per output in k order), otherwise to
+    ``gemv(x[b], ...)``."""
+    _dev(x, qweight, qsz, bias, out)
+    if x.dtype != torch.float16 or x.dim() not in (2, 3) or x.shape[-1] != K:
+        raise ValueError(f"x must be fp16 [B, M, {K}] or [M, {K}], got {x.dtype} {tuple(x.shape)}")
+    B = qweight.shape[0] if qweight.dim() == 5 else -1
+    shared_x = x.dim() == 2
+    M = x.shape[0] if shared_x else x.shape[1]
+    if not shared_x and x.shape[0] != B:
+        raise ValueError(f"x has {x.shape[0]} problems, qweight {B}")
+    if tuple(qweight.shape) != (B, *packed_shape(N, K, bits)) or qweight.dtype != torch.int32:
+        raise ValueError(f"qweight must be int32 {(B, *packed_shape(N, K, bits))}")
+    if tuple(qsz.shape) != (B, *sz_shape(N, K, group)) or qsz.dtype != torch.int32:
+        raise ValueError(f"qsz must be int32 {(B, *sz_shape(N, K, group))}")
+    if bias is not None and (bias.dtype != torch.float16 or tuple(bias.shape) != (B, N)):
+        raise ValueError("bias must be fp16 [B, N]")
+    y = out if out is not None else torch.empty(B, M, N, dtype=torch.float16, device=x.device)
+    if tuple(y.shape) != (B, M, N) or y.dtype != torch.float16:
+        raise ValueError(f"out must be fp16 [{B}, {M}, {N}]")
+    if B == 0 or M == 0:
+        return y
+    rc = load_library().qlin_gemv_batched_f16(
+        _ptr(qweight), qweight[0].numel(), _ptr(qsz), qsz[0].numel(), flags, _ptr(x),
+        0 if shared_x else M * K,
+        _ptr(bias), N, _ptr(y), M * N, B, M, N, K, bits, group, _stream(x))
+    _check(rc, "qlin_gemv_batched_f16")
+    return y
 
 
 def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0, split=True):

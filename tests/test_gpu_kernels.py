@@ -327,3 +327,69 @@ def test_gemv_two_row_tiles_per_block(N):
                              residual=t(r))
         ref = t(r) + qlin.gemv(t(x), qw, qsz, None, N, K, 4, group, fl)
         assert torch.equal(got, ref)
+
+
+# (batch, N, K, bits, group, M): fast-path problems (one launch, grid Nt x batch) and ones the
+# fast path does not take (14336-deep: > 4 tiles per wave; M > 4; K % 128) -> one launch each
+BATCHED_CASES = [(3, 4096, 4096, 4, 128, 1), (4, 777, 768, 3, 64, 2), (2, 300, 3072, 2, 64, 4),
+                 (3, 1040, 4096, 8, 128, 3), (2, 130, 14336, 4, 128, 1), (2, 64, 32, 4, 32, 13),
+                 (5, 96, 4096, 4, 4096, 1),
+                 # more tile rows than resident waves: several rows per wave, uneven split; Kt = 4
+                 # (the 4-deep prefetch instance) and Kt = 8
+                 (20, 4112, 512, 4, 128, 1), (20, 4096, 1024, 4, 64, 2)]
+
+
+@pytest.mark.parametrize("case", BATCHED_CASES)
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_gemv_batched_bit_identical_to_per_problem(case, with_bias):
+    """qlin_gemv_batched_f16: every y[b] within the GEMV tolerance of the oracle's x @ W_dq^T;
+    bit-identical to qlin_gemm_f16 (unsplit: one MFMA chain per output in k order) where the
+    streaming kernel runs (M <= 4, whole 128-k tiles), to qlin_gemv_f16 where the batch falls back
+    to one launch per problem."""
+    B, N, K, bits, group, M = case
+    packs = [_packed(N, K, bits, group, seed=17 * b + N) for b in range(B)]
+    fl = packs[0][2]
+    packs = [p for p in packs if p[2] == fl]  # one layout flag per batch
+    B = len(packs)
+    qw = torch.stack([p[0] for p in packs])
+    qsz = torch.stack([p[1] for p in packs])
+    x = np.stack([rand_x(M, K, seed=100 + b) for b in range(B)])
+    bias = (np.random.RandomState(5).randn(B, N) * 0.1).astype(np.float16) if with_bias else None
+    y = qlin.gemv_batched(t(x), qw, qsz, None if bias is None else t(bias), N, K, bits, group, fl)
+    stream = M <= 4 and K % 128 == 0
+    for b in range(B):
+        bb = None if bias is None else t(bias[b])
+        if stream:
+            yb = qlin.gemm(t(x[b]), qw[b], qsz[b], bb, N, K, bits, group, fl, split=False)
+        else:
+            yb = qlin.gemv(t(x[b]), qw[b], qsz[b], bb, N, K, bits, group, fl)
+        assert bit_equal(n(y[b]), n(yb)), f"problem {b}"
+        ref = O.linear_ref(x[b], packs[b][3], None if bias is None else bias[b])
+        assert_close_to_ref(n(y[b]), ref, what=f"batched b{bits} N{N} K{K} problem {b}")
+
+
+def test_gemv_batched_shared_activation():
+    """x_stride 0: several matrices applied to one activation (e.g. the reference's separate
+    gate_proj / up_proj modules on the same normed hidden state)."""
+    N, K, bits, group = 1024, 4096, 4, 128
+    packs = [_packed(N, K, bits, group, seed=40 + b) for b in range(3)]
+    qw = torch.stack([p[0] for p in packs])
+    qsz = torch.stack([p[1] for p in packs])
+    x = rand_x(1, K, seed=9)
+    y = qlin.gemv_batched(t(x), qw, qsz, None, N, K, bits, group, packs[0][2])
+    for b in range(3):
+        yb = qlin.gemm(t(x), qw[b], qsz[b], None, N, K, bits, group, packs[b][2], split=False)
+        assert bit_equal(n(y[b]), n(yb)), f"problem {b}"
+
+
+def test_gemv_batched_rejects_overlapping_strides():
+    lib = qlin.load_library()
+    qw, qsz, fl, _ = _packed(64, 256, 4, 128, seed=1)
+    x = torch.zeros(2, 1, 256, dtype=torch.float16, device="cuda")
+    y = torch.zeros(2, 1, 64, dtype=torch.float16, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    ok = lib.qlin_gemv_batched_f16(qw.data_ptr(), 0, qsz.data_ptr(), 0, fl, x.data_ptr(), 256,
+                                   None, 0, y.data_ptr(), 64, 2, 1, 64, 256, 4, 128, st)
+    assert ok == 1  # zero weight strides would alias problems
+    with pytest.raises(ValueError):
+        qlin.gemv_batched(x, qw.unsqueeze(0), qsz.unsqueeze(0), None, 64, 256, 4, 128, fl)

@@ -62,6 +62,12 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert lib.qlin_pack_codes(None, 16, 64, 4, None, None) == 1
     assert lib.qlin_pack_codes(p, 16, 48, 4, p, None) == 1  # K % 32
     assert lib.qlin_pack_codes(p, 16, 64, 5, p, None) == 1  # bits
+    gb = lib.qlin_gemv_batched_f16
+    assert gb(None, 0, None, 0, 0, None, 0, None, 0, None, 0, 2, 1, 16, 128, 4, 128, None) == 1
+    assert gb(p, 255, p, 16, 0, p, 128, None, 0, p, 16, 2, 1, 16, 128, 4, 128, None) == 1  # qw
+    assert gb(p, 256, p, 16, 0, p, 127, None, 0, p, 16, 2, 1, 16, 128, 4, 128, None) == 1  # x
+    assert gb(p, 256, p, 16, 0, p, 128, p, 8, p, 16, 2, 1, 16, 128, 4, 128, None) == 1  # bias
+    assert gb(p, 256, p, 16, 0, p, 128, None, 0, p, 16, 70000, 1, 16, 128, 4, 128, None) == 1
     assert lib.qlin_gemm_block_cols(0, 16, 4) == -1 and lib.qlin_gemm_block_cols(16, 16, 5) == -1
     assert lib.qlin_error_string(1) == b"invalid argument"
 

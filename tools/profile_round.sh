@@ -25,9 +25,16 @@ export TMPDIR=/tmp
 (cd /tmp && step kernel_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run \
    -- python "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline) || exit $?
 find "$OUT/kt" -name "*kernel_stats.csv" -exec cp {} "$OUT/${R}_gemv_int4_g128_kernel_stats.csv" \;
+# FETCH_SIZE per dispatch, one pass per mode: the batched streaming launch (headline) and the
+# dependent single launches (other_mode)
 (cd /tmp && step pmc 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run \
-   -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $?
-python tools/pmc_traffic.py "$OUT/pmc" gemv_ gemv_int4_g128 "$OUT/${R}_gemv_int4_g128_pmc.json"
+   -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode) || exit $?
+python tools/pmc_traffic.py "$OUT/pmc" gemv_stream gemv_int4_g128_batched \
+  "$OUT/${R}_gemv_int4_g128_batched_pmc.json"
+(cd /tmp && step pmc_launches 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcl" \
+   -o run -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode \
+   --mode launches) || exit $?
+python tools/pmc_traffic.py "$OUT/pmcl" gemv_fast gemv_int4_g128 "$OUT/${R}_gemv_int4_g128_pmc.json"
 step decode_layer 300 python tools/bench_decode.py
 step attn_prefill 300 python tools/dev/attn_prefill_bench.py
 step ppl_llama3_8b 500 python tools/ppl_llama3_8b.py
