@@ -95,6 +95,8 @@ def parse():
                          "(the decode chain's per-launch cost); the other mode is timed too and "
                          "reported beside it")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--ramp-s", type=float, default=0.3,
+                    help="untimed seconds of runs before the warmup steps (GPU clock ramp)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-mode", action="store_true",
                     help="skip timing the other GEMV mode (batched / launches)")
@@ -262,7 +264,13 @@ def main():
 
     def timed(run, steps, warmup):
         """HIP events on the launch stream around `steps` runs; barrier + synchronize on both
-        sides; MAX over ranks."""
+        sides; MAX over ranks.  Before the `warmup` steps, untimed runs for >= --ramp-s seconds
+        bring the GPU clock up from idle (a 0.1 ms step measured 20 % slow for the first ~20 ms
+        of work: tools/dev/batch_geo.py rep 1 vs reps 2-3)."""
+        t_ramp = time.perf_counter()
+        while time.perf_counter() - t_ramp < args.ramp_s:
+            run()
+            torch.cuda.synchronize(dev)
         for _ in range(warmup):
             run()
         torch.cuda.synchronize(dev)

@@ -344,7 +344,7 @@ BATCHED_CASES = [(3, 4096, 4096, 4, 128, 1), (4, 777, 768, 3, 64, 2), (2, 300, 3
 def test_gemv_batched_bit_identical_to_per_problem(case, with_bias):
     """qlin_gemv_batched_f16: every y[b] within the GEMV tolerance of the oracle's x @ W_dq^T;
     bit-identical to qlin_gemm_f16 (unsplit: one MFMA chain per output in k order) where the
-    streaming kernel runs (M <= 4, whole 128-k tiles), to qlin_gemv_f16 where the batch falls back
+    streaming kernel runs (M <= 4, K % 512 == 0), to qlin_gemv_f16 where the batch falls back
     to one launch per problem."""
     B, N, K, bits, group, M = case
     packs = [_packed(N, K, bits, group, seed=17 * b + N) for b in range(B)]
@@ -356,7 +356,7 @@ def test_gemv_batched_bit_identical_to_per_problem(case, with_bias):
     x = np.stack([rand_x(M, K, seed=100 + b) for b in range(B)])
     bias = (np.random.RandomState(5).randn(B, N) * 0.1).astype(np.float16) if with_bias else None
     y = qlin.gemv_batched(t(x), qw, qsz, None if bias is None else t(bias), N, K, bits, group, fl)
-    stream = M <= 4 and K % 128 == 0
+    stream = M <= 4 and K % 512 == 0
     for b in range(B):
         bb = None if bias is None else t(bias[b])
         if stream:
