@@ -51,6 +51,9 @@ constexpr int kStreamWaves = 4;
 #ifndef GEMV_STREAM_PF  // tiles in flight per wave (dev knob)
 #define GEMV_STREAM_PF 8
 #endif
+#ifndef GEMV_STREAM_ABLATE  // dev ablation (wrong results): 1 = no x loads / LDS park, 2 = constant
+#define GEMV_STREAM_ABLATE 0  // (scale, zero) words (loads and group decode folded), 3 = both
+#endif
 #ifndef GEMV_STREAM_PERSIST  // dev A/B knob: 0 = one tile row per wave (grid of T waves)
 #define GEMV_STREAM_PERSIST 1
 #endif
@@ -93,7 +96,13 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
     wt[u].pc = load_piece_nt<BITS>(lqw + kt * (64 * BITS));
     const int g0 = group_of_tile(kt);
 #pragma unroll
-    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = lsz[(g0 + s) * kTileN];
+    for (int s = 0; s < GPT; ++s)
+      wt[u].sz[s] = (GEMV_STREAM_ABLATE & 2) ? 0x3c000004u + (uint32_t)s : lsz[(g0 + s) * kTileN];
+    if (GEMV_STREAM_ABLATE & 1) {
+#pragma unroll
+      for (int c = 0; c < MT; ++c) xq[u].w[c] = 0x3c003c00u + (uint32_t)kt;
+      return;
+    }
     const _Float16* p = lx + kt * kTileK;
     if constexpr (MT == 1) {
       xq[u].w[0] = *reinterpret_cast<const uint32_t*>(p);
@@ -110,7 +119,13 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
   uint32_t* slot = &xs[wave][0];
   auto tile = [&](int u) {
     h8 xa[4];
-    park_x<MT>(xa, xq[u], slot, lane, n_in);
+    if (GEMV_STREAM_ABLATE & 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        xa[c] = __builtin_bit_cast(h8, make_uint4(xq[u].w[0], xq[u].w[0] + c, xq[u].w[0], 0u));
+    } else {
+      park_x<MT>(xa, xq[u], slot, lane, n_in);
+    }
     auto step = [&](auto S_) {
       constexpr int S = decltype(S_)::value;
       uint32_t v[4];

@@ -3,7 +3,7 @@
 Loads the product library (ring setup, reference output) and each tools/dev/libgs<P>_<PF>.so variant
 (GEMV_STREAM_PERSIST / GEMV_STREAM_PF) through ctypes, times one strided-batch launch over a ring of R 4096^2 int4
 g128 matrices (graph-replayed, HIP events), checks every variant bit-identical to the product.
-Usage: python tools/dev/batch_geo.py [R] [N] [K]
+Usage: python tools/dev/batch_geo.py [R] [N] [K] [bits] [group]
 """
 import ctypes
 import glob
@@ -18,7 +18,9 @@ from quant import qlin  # noqa: E402
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 K = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
-bits, group, M = 4, 128, 1
+bits = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+group = int(sys.argv[5]) if len(sys.argv) > 5 else 128
+M = 1
 dev = torch.device("cuda", 0)
 lib = qlin.load_library()
 qw = torch.zeros((R, *qlin.packed_shape(N, K, bits)), dtype=torch.int32, device=dev)
@@ -74,6 +76,6 @@ for rep in range(3):
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / steps
-        print(f"{name:14s} R={R} {N}x{K}: {us:8.2f} us/launch  {us / R:6.3f} us/matrix  "
+        print(f"{name:14s} R={R} {N}x{K} b{bits} g{group}: {us:8.2f} us/launch  {us / R:6.3f} us/matrix  "
               f"{nbytes / us / 1e3:7.1f} GB/s  {nbytes / us / 1e3 / 8000:.3f}  bit-identical={same}",
               flush=True)
