@@ -54,13 +54,28 @@ constexpr int kStreamWaves = 4;
 #ifndef GEMV_STREAM_ABLATE  // dev ablation (wrong results): 1 = no x loads / LDS park, 2 = constant
 #define GEMV_STREAM_ABLATE 0  // (scale, zero) words (loads and group decode folded), 3 = both
 #endif
+#ifndef GEMV_STREAM_SZR  // round-wide (scale, zero) loads (dev A/B knob)
+#define GEMV_STREAM_SZR 1
+#endif
+#ifndef GEMV_STREAM_PFS  // tiles in flight per wave for 2/3-bit tiles (dev knob)
+#define GEMV_STREAM_PFS 8
+#endif
 #ifndef GEMV_STREAM_PERSIST  // dev A/B knob: 0 = one tile row per wave (grid of T waves)
 #define GEMV_STREAM_PERSIST 1
 #endif
 
-template <int BITS, int MT, int GPT, int ZM, int PF>
+// SZR (group = 128 / GPT, i.e. 32, 64 or 128): the (scale, zero) words of a whole round of PF
+// tiles -- PF * GPT groups x 16 rows, contiguous in the qsz layout -- arrive as ONE 16-B-per-lane
+// load per 1 KB (one round ahead, like the codes) and are parked in the wave's LDS slot, from
+// where each k-step reads its lane's word, instead of GPT 64-byte loads per tile: fewer vector
+// memory instructions per tile (int2 g64: 4 -> 2 + 1/round).  tools/dev/batch_geo.py, one box,
+// best of 3: int2 g64 131 -> 125 us, int3 g64 116 -> 115, int4 g128 97.9 -> 96.7 (bit-identical).
+template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
 __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[kStreamWaves][64 * MT];
+  constexpr int SW = PF * GPT * kTileN;         // SZR: (scale, zero) words per round
+  constexpr int NC = SW >= 256 ? SW / 256 : 1;  // 16-B loads per lane per round
+  __shared__ __attribute__((aligned(16))) uint32_t szs[SZR ? kStreamWaves : 1][SZR ? SW : 4];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
@@ -77,13 +92,13 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
   int64_t lr = r0;
   int lkt = 0;
   const uint32_t* lqw;
-  const uint32_t* lsz;
+  const uint32_t* lsz;   // SZR: the row tile's qsz base; else + n_in
   const _Float16* lx;
   auto set_row = [&](int64_t r) {
     const int64_t b = r / a.Nt;
     const int nt = (int)(r - b * a.Nt);
     lqw = a.qw + b * a.bs_qw + (int64_t)nt * a.Kt * (64 * BITS) + lane * BITS;
-    lsz = a.qsz + b * a.bs_sz + (int64_t)nt * a.G * kTileN + n_in;
+    lsz = a.qsz + b * a.bs_sz + (int64_t)nt * a.G * kTileN + (SZR ? 0 : n_in);
     lx = a.x + b * a.bs_x + xlane;
   };
   set_row(lr);
@@ -92,12 +107,31 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
   };
   WTile<BITS, GPT> wt[PF];
   XRaw<MT> xq[PF];
+  uint4 szr[NC];  // SZR: the next round's (scale, zero) words, lane l: words 4l .. 4l + 3
+  auto load_szr = [&](int kt0) {  // round starting at tile kt0: groups kt0 * GPT ..
+    if constexpr (SZR) {
+      const uint32_t* p = lsz + kt0 * GPT * kTileN;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        szr[c] = *reinterpret_cast<const uint4*>(p + 256 * c + (4 * lane) % (SW < 256 ? SW : 256));
+    }
+  };
+  uint32_t* sslot = &szs[SZR ? wave : 0][0];
+  auto park_sz = [&] {
+    if constexpr (SZR) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        *reinterpret_cast<uint4*>(sslot + 256 * c + (4 * lane) % (SW < 256 ? SW : 256)) = szr[c];
+    }
+  };
   auto load = [&](int u, int kt) {
     wt[u].pc = load_piece_nt<BITS>(lqw + kt * (64 * BITS));
-    const int g0 = group_of_tile(kt);
+    if constexpr (!SZR) {
+      const int g0 = group_of_tile(kt);
 #pragma unroll
-    for (int s = 0; s < GPT; ++s)
-      wt[u].sz[s] = (GEMV_STREAM_ABLATE & 2) ? 0x3c000004u + (uint32_t)s : lsz[(g0 + s) * kTileN];
+      for (int s = 0; s < GPT; ++s)
+        wt[u].sz[s] = (GEMV_STREAM_ABLATE & 2) ? 0x3c000004u + (uint32_t)s : lsz[(g0 + s) * kTileN];
+    }
     if (GEMV_STREAM_ABLATE & 1) {
 #pragma unroll
       for (int c = 0; c < MT; ++c) xq[u].w[c] = 0x3c003c00u + (uint32_t)kt;
@@ -129,7 +163,9 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
     auto step = [&](auto S_) {
       constexpr int S = decltype(S_)::value;
       uint32_t v[4];
-      const GroupQ gq = make_group_w<BITS, ZM>(wt[u].sz[S * GPT / 4]);
+      const uint32_t szw =
+          SZR ? sslot[(u * GPT + S * GPT / 4) * kTileN + n_in] : wt[u].sz[S * GPT / 4];
+      const GroupQ gq = make_group_w<BITS, ZM>(szw);
       dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
       const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
@@ -159,17 +195,20 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
 
   // rounds of PF tiles (Kt % PF == 0: a round never straddles two tile rows); every round but
   // the last refills each slot right after computing it with the next round's tile
+  load_szr(0);
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u, u);
   int64_t cr = r0;  // compute stream: tile row, round start
   int ckt = 0;
   const int64_t rounds = (r1 - r0) * (a.Kt / PF);
   for (int64_t q = 0; q + 1 < rounds; ++q) {
+    park_sz();  // this round's (scale, zero) words into the wave's LDS slot
     lkt += PF;
     if (lkt == a.Kt) {  // wave-uniform
       lkt = 0;
       set_row(++lr);
     }
+    load_szr(lkt);
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       tile(u);
@@ -182,6 +221,7 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
       ++cr;
     }
   }
+  park_sz();
 #pragma unroll
   for (int u = 0; u < PF; ++u) tile(u);
   store(cr);
@@ -214,9 +254,9 @@ int stream_cu_count() {
   return n;
 }
 
-template <int BITS, int MT, int GPT, int ZM, int PF>
+template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
 int launch_stream_pf(StreamArgs a, hipStream_t st) {
-  auto k = gemv_stream_kernel<BITS, MT, GPT, ZM, PF>;
+  auto k = gemv_stream_kernel<BITS, MT, GPT, ZM, PF, SZR>;
   int64_t Wt = a.T;
   if (GEMV_STREAM_PERSIST)
     Wt = std::min<int64_t>(a.T, (int64_t)stream_cu_count() * blocks_per_cu(k) * kStreamWaves);
@@ -227,10 +267,24 @@ int launch_stream_pf(StreamArgs a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// tiles in flight per wave: GEMV_STREAM_PF for int4 / int8, GEMV_STREAM_PFS for the 2/3-bit tiles
+// (half / three quarters of the bytes per tile; 16 measured 5-10 % slower than 8 for them:
+// 8 more VGPR slots cost a wave per SIMD)
+template <int BITS, int MT, int GPT, int ZM, bool SZR>
+int launch_stream_s(const StreamArgs& a, hipStream_t st) {
+  constexpr int PF = BITS >= 4 ? GEMV_STREAM_PF : GEMV_STREAM_PFS;
+  if (a.Kt % PF == 0) return launch_stream_pf<BITS, MT, GPT, ZM, PF, SZR>(a, st);
+  if (PF > 8 && a.Kt % 8 == 0) return launch_stream_pf<BITS, MT, GPT, ZM, 8, SZR>(a, st);
+  return launch_stream_pf<BITS, MT, GPT, ZM, 4, SZR>(a, st);  // Kt % 4 == 0 (host)
+}
+
+// group = 128 / GPT: round-wide (scale, zero) loads; GPT == 1 with group > 128 (a multiple of
+// 128, per-channel included): per-tile loads (one group covers several tiles)
 template <int BITS, int MT, int GPT, int ZM>
 int launch_stream_t(const StreamArgs& a, hipStream_t st) {
-  if (a.Kt % GEMV_STREAM_PF == 0) return launch_stream_pf<BITS, MT, GPT, ZM, GEMV_STREAM_PF>(a, st);
-  return launch_stream_pf<BITS, MT, GPT, ZM, 4>(a, st);  // Kt % 4 == 0 (host)
+  if (GEMV_STREAM_SZR && (GPT > 1 || a.K / a.G == kTileK))
+    return launch_stream_s<BITS, MT, GPT, ZM, GEMV_STREAM_SZR != 0>(a, st);
+  return launch_stream_s<BITS, MT, GPT, ZM, false>(a, st);
 }
 
 }  // namespace

@@ -336,7 +336,10 @@ BATCHED_CASES = [(3, 4096, 4096, 4, 128, 1), (4, 777, 768, 3, 64, 2), (2, 300, 3
                  (5, 96, 4096, 4, 4096, 1),
                  # more tile rows than resident waves: several rows per wave, uneven split; Kt = 4
                  # (the 4-deep prefetch instance) and Kt = 8
-                 (20, 4112, 512, 4, 128, 1), (20, 4096, 1024, 4, 64, 2)]
+                 (20, 4112, 512, 4, 128, 1), (20, 4096, 1024, 4, 64, 2),
+                 # round-wide (scale, zero) loads: g32 (two 1-KB loads per round), g64 with 4-deep
+                 # rounds (lanes wrap over 512 B); group 256 keeps per-tile loads
+                 (3, 528, 1024, 4, 32, 1), (4, 1040, 512, 2, 64, 1), (3, 272, 2048, 3, 256, 2)]
 
 
 @pytest.mark.parametrize("case", BATCHED_CASES)
