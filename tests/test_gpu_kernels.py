@@ -385,6 +385,27 @@ def test_gemv_batched_shared_activation():
         assert bit_equal(n(y[b]), n(yb)), f"problem {b}"
 
 
+def test_gemv_batched_empty_and_shared_bias():
+    N, K, bits, group = 64, 1024, 4, 128
+    qw, qsz, fl, wdq = _packed(N, K, bits, group, seed=3)
+    x = torch.zeros(0, 1, K, dtype=torch.float16, device="cuda")
+    y = qlin.gemv_batched(x, qw[None][:0], qsz[None][:0], None, N, K, bits, group, fl)
+    assert tuple(y.shape) == (0, 1, N)
+    # bias_stride 0 through the C entry: one bias row shared by both problems
+    lib = qlin.load_library()
+    xs = t(np.stack([rand_x(1, K, seed=s_) for s_ in (1, 2)]))
+    b = t((np.random.RandomState(4).randn(N) * 0.1).astype(np.float16))
+    qw2, qsz2 = torch.stack([qw, qw]), torch.stack([qsz, qsz])
+    y2 = torch.empty(2, 1, N, dtype=torch.float16, device="cuda")
+    rc = lib.qlin_gemv_batched_f16(qw2.data_ptr(), qw.numel(), qsz2.data_ptr(), qsz.numel(), fl,
+                                   xs.data_ptr(), K, b.data_ptr(), 0, y2.data_ptr(), N, 2, 1, N, K,
+                                   bits, group, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    for i in range(2):
+        ref = qlin.gemm(xs[i], qw, qsz, b, N, K, bits, group, fl, split=False)
+        assert bit_equal(n(y2[i]), n(ref))
+
+
 def test_gemv_batched_rejects_overlapping_strides():
     lib = qlin.load_library()
     qw, qsz, fl, _ = _packed(64, 256, 4, 128, seed=1)
