@@ -60,6 +60,9 @@ constexpr int kStreamWaves = 4;
 #ifndef GEMV_STREAM_PFS  // tiles in flight per wave for 2/3-bit tiles (dev knob)
 #define GEMV_STREAM_PFS 8
 #endif
+#ifndef GEMV_STREAM_WPE_SUB  // minimum waves per SIMD asked of the 2/3-bit instances (dev knob;
+#define GEMV_STREAM_WPE_SUB 1   // 1 = compiler's choice)
+#endif
 #ifndef GEMV_STREAM_PERSIST  // dev A/B knob: 0 = one tile row per wave (grid of T waves)
 #define GEMV_STREAM_PERSIST 1
 #endif
@@ -71,7 +74,9 @@ constexpr int kStreamWaves = 4;
 // memory instructions per tile (int2 g64: 4 -> 2 + 1/round).  tools/dev/batch_geo.py, one box,
 // best of 3: int2 g64 131 -> 125 us, int3 g64 116 -> 115, int4 g128 97.9 -> 96.7 (bit-identical).
 template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
-__global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const StreamArgs a) {
+__global__ __launch_bounds__(64 * kStreamWaves)
+__attribute__((amdgpu_waves_per_eu(BITS < 4 ? GEMV_STREAM_WPE_SUB : 1)))
+void gemv_stream_kernel(const StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[kStreamWaves][64 * MT];
   constexpr int SW = PF * GPT * kTileN;         // SZR: (scale, zero) words per round
   constexpr int NC = SW >= 256 ? SW / 256 : 1;  // 16-B loads per lane per round
