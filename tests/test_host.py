@@ -125,6 +125,11 @@ def test_no_cpu_fallback():
     q = UniformAffineQuantizer(n_bits=4, group_size=32, dynamic_method="per_channel")
     with pytest.raises(RuntimeError, match="gfx950"):
         q(torch.randn(4, 64).half())
+    from quant import qlin
+    qw = torch.zeros(2, *qlin.packed_shape(16, 128, 4), dtype=torch.int32)
+    qsz = torch.zeros(2, *qlin.sz_shape(16, 128, 128), dtype=torch.int32)
+    with pytest.raises(RuntimeError, match="gfx950"):
+        qlin.gemv_batched(torch.zeros(2, 1, 128).half(), qw, qsz, None, 16, 128, 4, 128)
 
 
 def test_product_path_never_imports_the_oracle():
