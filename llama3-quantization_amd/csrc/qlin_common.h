@@ -378,6 +378,10 @@ int gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint1
             int64_t K, int bits, int group, int epilogue, int act_bits, int act_flags,
             void* stream);
 
+// CUs of the current device, cached per device id (qlin_gemm.hip; used by the GEMM's block-width
+// picker and the batched GEMV's resident-grid size)
+int device_cu_count();
+
 // torch's fp32 silu (x / (1 + exp(-x))) on an fp16 value, rounded to fp16
 __device__ __forceinline__ float silu_rn16(float g) {
 #pragma clang fp contract(off)

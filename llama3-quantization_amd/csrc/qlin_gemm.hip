@@ -439,21 +439,7 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   return (int)hipGetLastError();
 }
 
-// CUs of the current device, cached per device id (the first call per device queries it; racing
-// first calls store the same value)
-int cu_count() {
-  constexpr int kMaxDev = 64;
-  static std::atomic<int> cache[kMaxDev];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
-  int n = dev < kMaxDev ? cache[dev].load(std::memory_order_relaxed) : 0;
-  if (n > 0) return n;
-  int c = 0;
-  n = (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-       c > 0) ? c : 256;
-  if (dev < kMaxDev) cache[dev].store(n, std::memory_order_relaxed);
-  return n;
-}
+int cu_count() { return qlin::device_cu_count(); }
 
 // Block width.  The 128 x 256 / 384 / 512 blocks use 2 x 48-72 KB of LDS stages, so one block
 // fits a CU and a launch runs in rounds of `CUs` blocks.  Cost model fitted on int4 g128
@@ -685,4 +671,20 @@ extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, 
   }
   return gemm_ep(qweight, qsz, flags, x, bias, residual, y, M, N, K, bits, group, epilogue,
                  stream, workspace ? (void*)((char*)workspace + act_bytes) : nullptr);
+}
+
+// CUs of the current device, cached per device id (the first call per device queries it; racing
+// first calls store the same value)
+int qlin::device_cu_count() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  int n = dev < kMaxDev ? cache[dev].load(std::memory_order_relaxed) : 0;
+  if (n > 0) return n;
+  int c = 0;
+  n = (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+       c > 0) ? c : 256;
+  if (dev < kMaxDev) cache[dev].store(n, std::memory_order_relaxed);
+  return n;
 }

@@ -9,7 +9,6 @@
 #include "qlin_gemv_tile.h"
 
 #include <algorithm>
-#include <atomic>
 #include <type_traits>
 
 using namespace qlin;
@@ -244,27 +243,13 @@ int blocks_per_cu(Kern k) {
   return nb;
 }
 
-// CUs of the current device, cached per device id
-int stream_cu_count() {
-  constexpr int kMaxDev = 64;
-  static std::atomic<int> cache[kMaxDev];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
-  int n = dev < kMaxDev ? cache[dev].load(std::memory_order_relaxed) : 0;
-  if (n > 0) return n;
-  int c = 0;
-  n = (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-       c > 0) ? c : 256;
-  if (dev < kMaxDev) cache[dev].store(n, std::memory_order_relaxed);
-  return n;
-}
 
 template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
 int launch_stream_pf(StreamArgs a, hipStream_t st) {
   auto k = gemv_stream_kernel<BITS, MT, GPT, ZM, PF, SZR>;
   int64_t Wt = a.T;
   if (GEMV_STREAM_PERSIST)
-    Wt = std::min<int64_t>(a.T, (int64_t)stream_cu_count() * blocks_per_cu(k) * kStreamWaves);
+    Wt = std::min<int64_t>(a.T, (int64_t)device_cu_count() * blocks_per_cu(k) * kStreamWaves);
   a.Wt = Wt;
   const int64_t blocks = (Wt + kStreamWaves - 1) / kStreamWaves;
   a.xcd_chunk = blocks % 8 == 0 ? (int)(blocks / 8) : 0;
