@@ -62,6 +62,9 @@ constexpr int kStreamWaves = 4;
 #ifndef GEMV_STREAM_WPE_SUB  // minimum waves per SIMD asked of the 2/3-bit instances (dev knob;
 #define GEMV_STREAM_WPE_SUB 1   // 1 = compiler's choice)
 #endif
+#ifndef GEMV_STREAM_INTERLEAVE  // dev A/B knob: 1 = wave w takes tile rows w, w + Wt, ...
+#define GEMV_STREAM_INTERLEAVE 0
+#endif
 #ifndef GEMV_STREAM_PERSIST  // dev A/B knob: 0 = one tile row per wave (grid of T waves)
 #define GEMV_STREAM_PERSIST 1
 #endif
@@ -87,8 +90,12 @@ void gemv_stream_kernel(const StreamArgs a) {
   if (a.xcd_chunk > 0) blk = (blk & 7) * a.xcd_chunk + (blk >> 3);  // XCD j: a contiguous run
   const int64_t w = (int64_t)blk * kStreamWaves + wave;
   if (w >= a.Wt) return;  // wave-uniform; no barriers below
-  const int64_t r0 = w * a.T / a.Wt, r1 = (w + 1) * a.T / a.Wt;
-  if (r0 >= r1) return;
+  // tile rows of this wave: contiguous [wT/Wt, (w+1)T/Wt), or (dev knob) w, w + Wt, w + 2 Wt, ...
+  const int64_t rstep = GEMV_STREAM_INTERLEAVE ? a.Wt : 1;
+  const int64_t r0 = GEMV_STREAM_INTERLEAVE ? w : w * a.T / a.Wt;
+  const int64_t nrows = GEMV_STREAM_INTERLEAVE ? (a.T - w + a.Wt - 1) / a.Wt
+                                               : (w + 1) * a.T / a.Wt - r0;
+  if (nrows <= 0) return;
   constexpr int LPR = 64 / MT;
   const int xlane = min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
 
@@ -204,13 +211,14 @@ void gemv_stream_kernel(const StreamArgs a) {
   for (int u = 0; u < PF; ++u) load(u, u);
   int64_t cr = r0;  // compute stream: tile row, round start
   int ckt = 0;
-  const int64_t rounds = (r1 - r0) * (a.Kt / PF);
+  const int64_t rounds = nrows * (a.Kt / PF);
   for (int64_t q = 0; q + 1 < rounds; ++q) {
     park_sz();  // this round's (scale, zero) words into the wave's LDS slot
     lkt += PF;
     if (lkt == a.Kt) {  // wave-uniform
       lkt = 0;
-      set_row(++lr);
+      lr += rstep;
+      set_row(lr);
     }
     load_szr(lkt);
 #pragma unroll
@@ -222,7 +230,7 @@ void gemv_stream_kernel(const StreamArgs a) {
     if (ckt == a.Kt) {  // wave-uniform: the tile row is complete
       store(cr);
       ckt = 0;
-      ++cr;
+      cr += rstep;
     }
   }
   park_sz();
