@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 5
+#define QLIN_ABI_VERSION 6
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -73,7 +73,9 @@ const char* qlin_error_string(int code);
  * Fused RTN quantizer: per-group min/max calibration + fake-quant (+ optional packing), one pass.
  * Replaces UniformAffineQuantizer.forward -> per_token_dynamic_calibration -> fake_quant
  * (quant/quantizer.py:118-159, :94-115), bit-exact in the input dtype (fp16 or fp32).
- *   x          [rows, K] dtype;  group divides K (group = K: per-channel / per-token).
+ *   x          [rows, K] dtype;  group divides K (group = K: per-channel / per-token); K and
+ *              group multiples of 32, except one group per row (group == K) without packing,
+ *              which takes any K (QuantMatMul's per-token operands: K = the key count).
  *   lwc_up_sig, lwc_low_sig  [rows*K/group] dtype: sigmoid(upbound/lowbound_factor) (QLIN_LWC).
  *   x_dq       [rows, K] dtype or NULL;  scale_out / zp_out [rows*K/group] dtype or NULL
  *              (zp_out unused with QLIN_DISABLE_ZERO_POINT) — the reference's scale /
@@ -348,6 +350,56 @@ int qlin_rope_kv_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
 int qlin_attn_scores_f32(float* scores, const void* mask, int mask_dtype, int64_t B, int64_t H,
                          int64_t T, int64_t L, int64_t mask_batch_stride, float scale_div,
                          void* stream);
+
+/*
+ * Persistent decode engine: ONE launch runs one decode step — batch 1, one new token over a KV
+ * cache — through n_layers consecutive quantized LLaMA decoder layers.  Replaces, per layer,
+ * QuantLlamaDecoderLayer.forward at q_len == 1 (models/int_llama_layer.py:213-267 of the
+ * reference: RMSNorm, q/k/v QuantLinear, RoPE, KV append, attention, o_proj + residual, RMSNorm,
+ * gate/up QuantLinear + SiLU * up, down_proj + residual; every QuantLinear.forward =
+ * F.linear(x, W_dq), quant/int_linear.py:62).  Every CU streams its share of all the layers'
+ * packed weights continuously; the activations cross CUs through agent-scope hand-offs inside the
+ * launch (DESIGN.md §4 "decode engine").
+ *   layers  DEVICE array of n_layers qlin_decode_layer (the packed operands of each layer, all
+ *           with the same bits / group / flags; q/k/v rows concatenated as FusedPackedLinear,
+ *           gate/up interleaved in 8-row halves as qlin_linear_ep_f16's QLIN_EP_SILU_MUL layout);
+ *   x       fp16 [H] the first layer's input hidden state;  y  fp16 [H] the last layer's output;
+ *   caches  fp16 [Hkv, kv_rows, D] per layer, rows 0 .. L0 - 1 valid; the step writes the rotated k
+ *           and the v row at L0 and attends over L0 + 1 rows;
+ *   cos_cache, sin_cache  fp32 [cache_rows, D], position  int64 device scalar (as qlin_rope_f16);
+ *   mask    fp16 [L0 + 1] additive or NULL;  scale_div = sqrt(D);  eps  the RMSNorms' epsilon;
+ *   workspace  >= qlin_decode_workspace_bytes(n_layers, H, I, Hq, Hkv, D, L0 + 1) bytes, 256-B
+ *           aligned, owned by the caller, used by one launch at a time; its first int32 is 0 after
+ *           a completed step and nonzero if a cross-CU wait timed out (every wave then exits; y is
+ *           undefined) — the caller may read it back to check.
+ * Arithmetic: the GEMV tiles of qlin_gemv_f16 (exact W_dq, fp32 accumulation, fp16 outputs, the
+ * fp16 epilogues); a row whose k-tiles are split over waves is summed in k order; RMSNorm and
+ * attention as qlin_rmsnorm_linear_ep_f16 / qlin_attn_decode_rope (fp32).  Equal to the per-layer
+ * launches up to fp32 summation order.  Requires D == 128, Hq == H / D, Hq / Hkv <= 8,
+ * H <= 8192, I <= 16384 (both multiples of 128), L0 + 1 <= 4096, group a multiple of 128 or 64,
+ * no QLIN_WIDE_ZERO, and enough CUs that every phase has <= 8 tile rows per CU
+ * (qlin_decode_supported); every CU runs one 512-thread workgroup of the launch, so nothing else
+ * may occupy the device's CUs while it runs.
+ */
+typedef struct qlin_decode_layer {
+  const uint32_t* qweight[4]; /* q/k/v (fused), o_proj, gate/up (interleaved), down_proj */
+  const uint32_t* qsz[4];
+  const float* input_norm;    /* fp32 [H] RMSNorm weights */
+  const float* post_norm;
+  uint16_t* k_cache;          /* fp16 [Hkv, kv_rows, D] */
+  uint16_t* v_cache;
+} qlin_decode_layer;
+
+int qlin_decode_supported(int n_layers, int64_t H, int64_t I, int Hq, int Hkv, int D, int bits,
+                          int group, int flags);
+int64_t qlin_decode_workspace_bytes(int n_layers, int64_t H, int64_t I, int Hq, int Hkv, int D,
+                                    int64_t max_L);
+int qlin_decode_llama_f16(const void* layers, int n_layers, int64_t H, int64_t I, int Hq,
+                          int Hkv, int D, int bits, int group, int flags, float eps,
+                          const uint16_t* x, uint16_t* y, const float* cos_cache,
+                          const float* sin_cache, int64_t cache_rows, const int64_t* position,
+                          int64_t L0, int64_t kv_rows, const uint16_t* mask, float scale_div,
+                          void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

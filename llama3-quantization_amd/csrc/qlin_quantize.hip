@@ -282,6 +282,47 @@ __global__ __launch_bounds__(kThreads) void pack_codes_kernel(const uint8_t* __r
   pack_piece<BITS>(u, qweight + pc * BITS);
 }
 
+// one group per row of any length K (per-token activations, per-channel weights) without packing:
+// QuantMatMul's per-token operands have K = the key count L, not a multiple of 32.  One wave per
+// row: min / max (order-free, NaN-propagating: bit-exact), the reference calibration, fake-quant.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void rowq_kernel(const T* __restrict__ x, QP P,
+                                                        const T* __restrict__ up,
+                                                        const T* __restrict__ low,
+                                                        T* __restrict__ x_dq,
+                                                        T* __restrict__ scale_out,
+                                                        T* __restrict__ zp_out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (kThreads / 64) + wave;
+  if (row >= P.rows) return;
+  const T* xr = x + row * P.K;
+  float mn = __builtin_inff(), mx = -__builtin_inff();
+  for (int k = lane; k < P.K; k += 64) {
+    const float v = (float)xr[k];
+    mn = min_nan(mn, v);
+    mx = max_nan(mx, v);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    mn = min_nan(mn, __shfl_xor(mn, o));
+    mx = max_nan(mx, __shfl_xor(mx, o));
+  }
+  float upf = 1.f, lowf = 1.f;
+  if (P.flags & QLIN_LWC) { upf = (float)up[row]; lowf = (float)low[row]; }
+  float scale, zp;
+  calib<T>(mn, mx, upf, lowf, P, scale, zp);
+  const bool has_zp = !(P.flags & QLIN_DISABLE_ZERO_POINT);
+  if (lane == 0) {
+    if (scale_out) scale_out[row] = (T)scale;
+    if (zp_out && has_zp) zp_out[row] = (T)zp;
+  }
+  if (!x_dq) return;
+  for (int k = lane; k < P.K; k += 64) {
+    float xi;
+    x_dq[row * P.K + k] = (T)fq<T>((float)xr[k], scale, zp, has_zp, P, xi);
+  }
+}
+
 template <typename T>
 int launch_quantize(const void* x, int64_t rows, int64_t K, int bits, int group, int flags,
                     const void* up, const void* low, void* x_dq, void* scale_out, void* zp_out,
@@ -292,15 +333,20 @@ int launch_quantize(const void* x, int64_t rows, int64_t K, int bits, int group,
   P.group = group;
   P.cpr = (int)(K / 32);
   P.cpg = group / 32;
-  P.rpb = P.cpr >= kThreads ? 1 : kThreads / P.cpr;
+  P.rpb = P.cpr >= kThreads ? 1 : kThreads / (P.cpr > 0 ? P.cpr : 1);
   P.bits = bits;
   P.flags = flags;
   const bool has_zp = !(flags & QLIN_DISABLE_ZERO_POINT);
   P.qmin = has_zp ? 0.f : -(float)(1 << (bits - 1));
   P.qmax = has_zp ? (float)((1 << bits) - 1) : (float)((1 << (bits - 1)) - 1);
-  const dim3 grid((unsigned)((rows + P.rpb - 1) / P.rpb));
   const bool pack = qweight != nullptr;
   const T* xx = (const T*)x;
+  if (K % 32 || K / 32 > kMaxChunks) {  // one whole-row group, no packing (checked by the caller)
+    hipLaunchKernelGGL((rowq_kernel<T>), dim3((unsigned)((rows + 3) / 4)), dim3(kThreads), 0, st,
+                       xx, P, (const T*)up, (const T*)low, (T*)x_dq, (T*)scale_out, (T*)zp_out);
+    return (int)hipGetLastError();
+  }
+  const dim3 grid((unsigned)((rows + P.rpb - 1) / P.rpb));
 #define QLIN_Q(B)                                                                            \
   hipLaunchKernelGGL((quantize_kernel<T, B>), grid, dim3(kThreads), 0, st, xx, P,            \
                      (const T*)up, (const T*)low, (T*)x_dq, (T*)scale_out, (T*)zp_out,       \
@@ -328,11 +374,14 @@ extern "C" int qlin_quantize(const void* x, int dtype, int64_t rows, int64_t K, 
                              int group, int flags, const void* lwc_up_sig,
                              const void* lwc_low_sig, void* x_dq, void* scale_out, void* zp_out,
                              uint32_t* qweight, uint32_t* qsz, void* stream) {
-  if (!x || rows < 0 || K <= 0 || K % 32 || K / 32 > kMaxChunks || group <= 0 || group % 32 ||
-      K % group || bits < 2 || bits > 8 || (dtype != QLIN_F16 && dtype != QLIN_F32))
+  const bool pack = qweight || qsz;
+  // K % 32 != 0 (or K > 32768): only one group per row and no packing (rowq_kernel)
+  const bool rowwise = K > 0 && (K % 32 || K / 32 > kMaxChunks);
+  if (!x || rows < 0 || K <= 0 || K > (1 << 24) || group <= 0 || K % group || bits < 2 ||
+      bits > 8 || (dtype != QLIN_F16 && dtype != QLIN_F32) ||
+      (rowwise ? (group != K || pack) : group % 32 != 0))
     return QLIN_EINVAL;
   if ((flags & QLIN_LWC) && (!lwc_up_sig || !lwc_low_sig)) return QLIN_EINVAL;
-  const bool pack = qweight || qsz;
   if (pack && (!qweight || !qsz || dtype != QLIN_F16 ||
                !(bits == 2 || bits == 3 || bits == 4 || bits == 8)))
     return QLIN_EINVAL;

@@ -16,7 +16,7 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -68,6 +68,10 @@ SIGNATURES = {
     "qlin_attn_decode": ([_p, _p, _p, _p, _p, _i, _l, _i, _i, _l, _i, _l, ctypes.c_float, _p, _p,
                           _p],
                          _i),
+    "qlin_decode_supported": ([_i, _l, _l, _i, _i, _i, _i, _i, _i], _i),
+    "qlin_decode_workspace_bytes": ([_i, _l, _l, _i, _i, _i, _l], _l),
+    "qlin_decode_llama_f16": ([_p, _i, _l, _l, _i, _i, _i, _i, _i, _i, ctypes.c_float, _p, _p, _p,
+                               _p, _l, _p, _l, _l, _p, ctypes.c_float, _p, _l, _p], _i),
 }
 
 
@@ -726,19 +730,20 @@ def attn_prefill_supported(q, k, mask=None):
                                   and mask.dtype in (torch.float16, torch.float32))))
 
 
-_CAUSAL = {}
+_CAUSAL = []  # [(mask tensor, its _version, S, L, result)], most recent last
+_CAUSAL_KEEP = 4
 
 
 def mask_is_causal(mask, S, L) -> int:
     """1 if the additive mask [B', 1, S, L] leaves every key past a query's diagonal
     (key > L - S + i) at <= -1e4 (so its exp() underflows to 0) and keeps some key of every row
     open, 2 if moreover every key on and below the diagonal is exactly 0 (the pure causal
-    pattern), else 0; cached per tensor version (one check per forward: the decoder layers share
-    the mask)."""
-    key = (mask.data_ptr(), mask._version, tuple(mask.shape), tuple(mask.stride()), mask.dtype)
-    hit = _CAUSAL.get(key)
-    if hit is not None:
-        return hit
+    pattern), else 0.  Cached per tensor OBJECT and version (one check per forward: the decoder
+    layers share the mask): the cache holds the mask itself and matches it with ``is``, so a new
+    mask that the allocator places at a freed mask's address is never taken for it."""
+    for ent in _CAUSAL:
+        if ent[0] is mask and ent[1] == mask._version and ent[2] == S and ent[3] == L:
+            return ent[4]
     i = torch.arange(S, device=mask.device)[:, None]
     j = torch.arange(L, device=mask.device)[None, :]
     above = j > (L - S) + i
@@ -747,9 +752,8 @@ def mask_is_causal(mask, S, L) -> int:
     ok = int(bool((m[:, above] <= -1e4).all()) and bool((open_max > -1e4).all()))
     if ok and bool((m[:, ~above] == 0).all()):
         ok = 2
-    if len(_CAUSAL) > 64:
-        _CAUSAL.clear()
-    _CAUSAL[key] = ok
+    _CAUSAL.append((mask, mask._version, S, L, ok))
+    del _CAUSAL[:-_CAUSAL_KEEP]
     return ok
 
 
@@ -782,3 +786,32 @@ def attn_prefill(q, k, v, mask, scale_div, out_dtype=torch.float32):
                                           float(scale_div), _stream(q))
     _check(rc, "qlin_attn_prefill")
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# persistent decode engine (qlin_decode_llama_f16)
+# ---------------------------------------------------------------------------------------------
+DECODE_LAYER_PTRS = 12  # qlin_decode_layer: 4 qweight, 4 qsz, 2 norm weights, 2 caches
+
+
+def decode_supported(n_layers, H, I, Hq, Hkv, D, bits, group, flags) -> bool:
+    return bool(load_library().qlin_decode_supported(n_layers, H, I, Hq, Hkv, D, bits, group,
+                                                     flags))
+
+
+def decode_workspace_bytes(n_layers, H, I, Hq, Hkv, D, max_L) -> int:
+    return int(load_library().qlin_decode_workspace_bytes(n_layers, H, I, Hq, Hkv, D, max_L))
+
+
+def decode_llama(table, n_layers, H, I, Hq, Hkv, D, bits, group, flags, eps, x, y, cos_cache,
+                 sin_cache, position, L0, kv_rows, mask, scale_div, workspace):
+    """``qlin_decode_llama_f16``: one decode step through ``n_layers`` layers in one launch.
+    ``table`` int64 [n_layers, 12] device tensor of qlin_decode_layer pointers; x / y fp16 [H];
+    position int64 device scalar; mask fp16 [L0 + 1] or None; workspace uint8 device buffer."""
+    _on_gpu(table, x, y, cos_cache, sin_cache, position, mask, workspace)
+    rc = load_library().qlin_decode_llama_f16(
+        _ptr(table), n_layers, H, I, Hq, Hkv, D, bits, group, flags, float(eps), _ptr(x), _ptr(y),
+        _ptr(cos_cache), _ptr(sin_cache), cos_cache.shape[0], _ptr(position), L0, kv_rows,
+        _ptr(mask), float(scale_div), _ptr(workspace), workspace.numel(), _stream(x))
+    _check(rc, "qlin_decode_llama_f16")
+    return y

@@ -102,12 +102,15 @@ def test_pack_and_dequant_bit_exact(name):
 
 
 def _packed(N, K, bits, group, seed, wide=False):
+    """Packed operands from the HIP quantizer, and the ORACLE's W_dq of the same weight (the
+    reference's UniformAffineQuantizer arithmetic restated in numpy, oracle/quant_oracle.py
+    quantize): the product tests anchor on the reference's W_dq, not on the kernels' own dequant."""
     W = rand_weight(N, K, seed)
     if wide:
         W[: max(1, N // 7), :group] = 1.0 + np.random.RandomState(seed).rand(
             max(1, N // 7), group).astype(np.float16) * np.float16(1e-3)
     out = qlin.quantize(t(W), bits, group, 0, pack=True)
-    wdq = n(qlin.dequant(out["qweight"], out["qsz"], N, K, bits, group, out["flags"]))
+    wdq, *_ = O.quantize(W, bits, group)
     return out["qweight"], out["qsz"], out["flags"], wdq
 
 
@@ -279,6 +282,47 @@ def test_gemm_block_widths_bit_identical(bits, group):
                             split=False)
             assert torch.equal(big[:128], small), f"M={M} N={N} b{bits} g{group}"
     assert len(seen) >= 2, seen  # 256-CU MI355X: {255 (64 x 256), 256, 384, 512}
+
+
+def test_packed_operands_dequantize_to_the_oracle_wdq():
+    """The operands every product test uses: the HIP dequant of the packed weight equals the
+    oracle's W_dq bit for bit at LLaMA3-8B widths (4096^2, int4 g128 / int3 g64 / int2 g64)."""
+    for bits, group in ((4, 128), (3, 64), (2, 64)):
+        qw, qsz, fl, wdq = _packed(4096, 4096, bits, group, seed=bits)
+        got = n(qlin.dequant(qw, qsz, 4096, 4096, bits, group, fl))
+        assert bit_equal(got, wdq), f"b{bits} g{group}: {np.sum(got != wdq)} mismatches"
+
+
+def _sample_rows(M):
+    """Rows checked against the float64 product: both ends, the middle, and a spread of rows
+    (every 128-row block tile of the launch contributes some)."""
+    rs = np.random.RandomState(M)
+    rows = np.r_[0:64, M // 2 - 32:M // 2 + 32, M - 64:M, rs.randint(0, M, 192)]
+    return np.unique(rows.clip(0, M - 1))
+
+
+@pytest.mark.parametrize("M", [2048, 65536])
+def test_gemm_llama_shapes_configs2(M):
+    """BASELINE configs[2]: QuantLinear.forward with x [32, 2048, 4096] (M = 65,536; reference
+    quant/int_linear.py:48-65) and one 2048-token PPL window (M = 2048) on the int4 g128 4096^2
+    packed weight, through the product dispatch (qlin.linear), against the float64 product on the
+    oracle's W_dq for sampled rows; the whole output is finite and the launch deterministic."""
+    N = K = 4096
+    qw, qsz, fl, wdq = _packed(N, K, 4, 128, seed=M)
+    g = torch.Generator(device="cuda").manual_seed(M)
+    x = torch.empty(M, K, dtype=torch.float16, device="cuda").normal_(0, 1, generator=g)
+    shp = (32, 2048, K) if M == 65536 else (1, 2048, K)
+    y = qlin.linear(x.view(shp), qw, qsz, None, N, K, 4, 128, fl).view(M, N)
+    assert torch.isfinite(y).all()
+    rows = _sample_rows(M)
+    assert_close_to_ref(n(y[rows]), O.linear_ref(n(x[rows]), wdq), what=f"gemm M{M}")
+    y2 = qlin.linear(x.view(shp), qw, qsz, None, N, K, 4, 128, fl).view(M, N)
+    assert torch.equal(y, y2)
+    # the kernel reproduces F.linear(x, W_dq) (the fake-quant path's hipBLASLt GEMM) to fp16
+    # output rounding
+    ref = torch.nn.functional.linear(x[rows], t(wdq))
+    assert (y[rows].float() - ref.float()).abs().max().item() <= \
+        2e-3 * ref.float().abs().max().item()
 
 
 @pytest.mark.parametrize("M,N,K", [(65, 4096, 4096), (128, 4096, 14336), (200, 1040, 4096),

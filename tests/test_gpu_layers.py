@@ -80,12 +80,19 @@ def test_llama_layer_matches_reference():
     with torch.no_grad():
         y = q(x, attention_mask=mask, position_ids=pos)[0]
     assert rel_max_err(n(y), g["y_w4"]) < 1e-5
-    # packed gfx950 path, fp16 activations, vs the reference's fp32 output
+    # fp16 activations: the reference's own fake-quant path run in fp16 (dense F.linear on W_dq)
+    # sets the error budget of the packed path against the reference's fp32 output — the packed
+    # path may not be measurably worse than the reference arithmetic it replaces
     q.half()
+    xh, mh = x.half(), mask.half()
+    with torch.no_grad():
+        yf = q(xh, attention_mask=mh, position_ids=pos)[0]
+    err_fq = rel_max_err(n(yf), g["y_w4"])
     pack_quant_linears(q)
     with torch.no_grad():
-        yp = q(x.half(), attention_mask=mask.half(), position_ids=pos)[0]
-    assert rel_max_err(n(yp), g["y_w4"]) < 1e-2
+        yp = q(xh, attention_mask=mh, position_ids=pos)[0]
+    err_pk = rel_max_err(n(yp), g["y_w4"])
+    assert err_fq < 1e-2 and err_pk <= 1.25 * err_fq + 1e-4, (err_pk, err_fq)
 
 
 def test_llama_packed_equals_fake_quant_fp16():
@@ -126,3 +133,27 @@ def test_opt_layer_matches_reference(abits):
         y_pk = q(x.half(), attention_mask=mask.half())[0]
     assert rel_max_err(n(y_pk), n(y_fq)) < (1e-3 if abits == 16 else 5e-3)
     assert rel_max_err(n(y_pk), g["y_" + tag]) < 2e-2
+
+
+def test_quant_matmul_a8_matches_reference():
+    """QuantMatMul with per-token 8-bit activation quantizers on both operands (the reference's
+    quant_x1 / quant_x2 + matmul, quant/int_matmul.py:31-42) on the GPU: the HIP quantizer's
+    operands equal the oracle's bit for bit and the product equals the reference's own output
+    (tests/golden/mm_a8_f32.npz, written by importing the reference) to fp32 summation order."""
+    from oracle import quant_oracle as O
+    from quant.int_matmul import QuantMatMul
+    g = load_golden("mm_a8_f32")
+    qp = dict(n_bits=8, per_channel_axes=[], symmetric=False, dynamic_method="per_token")
+    mm = QuantMatMul(qp, qp, matmul_func=torch.matmul).cuda()
+    x1, x2 = t(g["x1"]), t(g["x2"])
+    with torch.no_grad():
+        y16 = mm(x1, x2)
+        mm.set_quant_state(False, True)
+        a, b = mm.quant_x1(x1), mm.quant_x2(x2)
+        y = mm(a, b)
+    np.testing.assert_allclose(n(y16), g["y"], rtol=1e-5, atol=1e-5)
+    ra, *_ = O.quantize(g["x1"], 8, None)
+    rb, *_ = O.quantize(g["x2"], 8, None)
+    assert np.array_equal(n(a).view(np.uint32), ra.view(np.uint32))
+    assert np.array_equal(n(b).view(np.uint32), rb.view(np.uint32))
+    np.testing.assert_allclose(n(y), g["y_a8"], rtol=1e-5, atol=1e-5)

@@ -132,6 +132,33 @@ def test_no_cpu_fallback():
         qlin.gemv_batched(torch.zeros(2, 1, 128).half(), qw, qsz, None, 16, 128, 4, 128)
 
 
+def test_mask_is_causal_cache_keys_on_the_tensor_object():
+    """A padded mask built after a causal mask of the same shape was freed (the allocator often
+    hands it the same address, and both start at _version 0) must be classified afresh."""
+    from quant import qlin
+    S = L = 8
+    minv = torch.finfo(torch.float16).min
+
+    def causal():
+        return torch.triu(torch.full((S, L), minv), 1).half()[None, None]
+
+    m = causal()
+    assert qlin.mask_is_causal(m, S, L) == 2
+    assert qlin.mask_is_causal(m, S, L) == 2  # cached
+    storage = m.untyped_storage()
+    del m
+    padded = causal()
+    padded[..., 1:, 0] = minv  # left padding: key 0 masked for query rows 1.. (row 0 keeps it)
+    assert qlin.mask_is_causal(padded, S, L) == 1
+    # the same object again after an in-place edit (version bump) is re-checked too
+    padded[..., 3, 5] = 0  # opens a key past the diagonal
+    assert qlin.mask_is_causal(padded, S, L) == 0
+    # a fresh tensor written into the freed storage (same address, _version 0)
+    reused = torch.empty(0, dtype=torch.float16).set_(storage).view(1, 1, S, L)
+    reused.fill_(0)
+    assert qlin.mask_is_causal(reused, S, L) == 0
+
+
 def test_product_path_never_imports_the_oracle():
     pkg = os.path.join(ROOT, "llama3-quantization_amd")
     for dirpath, _, files in os.walk(pkg):
