@@ -105,44 +105,51 @@ def parse():
 
 
 def cpu_baseline(M, N, K, bits, group, seconds):
-    """The reference's fake-quant CPU path, restated by the oracle (numpy), on the host cores.
-
-    Mode (ii) — what the reference runs at eval (weight == W_dq, dense F.linear): x @ W_dq^T over a
-    bounded sample of distinct pre-dequantized matrices (fp32 BLAS), repeated for ~``seconds``.
-    Mode (i) — quantize every call (use_weight_quant=True): oracle.quantize + the same product."""
-    import numpy as np
-    from oracle import quant_oracle as O
+    """The reference's fake-quant path on the host cores, restated in torch
+    (oracle/torch_ref.py, pinned bit-exactly to the reference's golden W_dq), with
+    torch.set_num_threads(<CPUs this process may run on>):
+      mode (ii) — what the reference runs at eval (weight == W_dq; quant/int_linear.py:62):
+               fp16 F.linear(x, W_dq) over a bounded sample of distinct pre-dequantized matrices;
+               value = median TFLOP/s of 5 timed runs after a warm-up;
+      mode (i)  — quantize every call (use_weight_quant=True, quant/quantizer.py:118-159 then
+               F.linear): median ms per call of >= 5 calls."""
+    import statistics
+    import torch
+    import torch.nn.functional as F
+    from oracle import torch_ref as TR
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
+        threads = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
         threads = os.cpu_count() or 1
-    rs = np.random.RandomState(0)
-    nmat = 4
-    mats = []
-    for i in range(nmat):
-        w = (rs.randn(N, K) * 0.02).astype(np.float16)
-        w_dq, *_ = O.quantize(w, bits, group)
-        mats.append(np.ascontiguousarray(w_dq.astype(np.float32)))
-    x = rs.randn(M, K).astype(np.float32)
-    y = mats[0] @ x.T  # warm
-    launches = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        for w in mats:
-            y = w @ x.T
-            launches += 1
-    dt = time.perf_counter() - t0
-    tflops = 2.0 * M * N * K * launches / dt / 1e12
-    w16 = (rs.randn(N, K) * 0.02).astype(np.float16)
-    t1 = time.perf_counter()
-    reps = 0
-    while time.perf_counter() - t1 < min(4.0, seconds / 3) or reps == 0:
-        w_dq, *_ = O.quantize(w16, bits, group)
-        y = w_dq.astype(np.float32) @ x.T
-        reps += 1
-    quant_ms = (time.perf_counter() - t1) / reps * 1e3
-    del y
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        g = torch.Generator().manual_seed(0)
+        nmat = 4
+        w16 = [(torch.randn(N, K, generator=g) * 0.02).half() for _ in range(nmat)]
+        wdq = [TR.quantize(w, bits, group)[0].contiguous() for w in w16]
+        x = torch.randn(M, K, generator=g).half()
+        F.linear(x, wdq[0])  # warm-up
+        runs, products = [], 0
+        per_run = max(0.2, 0.6 * seconds / 5)
+        for _ in range(5):
+            n = 0
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < per_run:
+                for w in wdq:
+                    F.linear(x, w)
+                    n += 1
+            dt = time.perf_counter() - t0
+            runs.append(2.0 * M * N * K * n / dt / 1e12)
+            products += n
+        calls = []
+        t1 = time.perf_counter()
+        while len(calls) < 5 or (time.perf_counter() - t1 < 0.3 * seconds and len(calls) < 50):
+            t0 = time.perf_counter()
+            TR.quant_linear(x, w16[len(calls) % nmat], bits, group)
+            calls.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
     cpu_model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -152,13 +159,16 @@ def cpu_baseline(M, N, K, bits, group, seconds):
                     break
     except OSError:
         pass
-    return {"value": round(tflops, 6), "unit": "TFLOP/s", "cores": int(threads), "kind": "port",
-            "cpu_model": cpu_model, "nproc": os.cpu_count(),
-            "sample": (f"oracle (numpy fp32 BLAS) x@W_dq^T, M={M} N={N} K={K}, {nmat} distinct "
-                       f"pre-dequantized int{bits} g{group} matrices cycled for {dt:.1f}s "
-                       f"({launches} products; reference eval mode ii)"),
-            "ms_per_product": round(dt / launches * 1e3, 4),
-            "quantize_every_call_ms": round(quant_ms, 2)}
+    return {"value": round(statistics.median(runs), 6), "unit": "TFLOP/s", "cores": int(threads),
+            "kind": "port", "cpu_model": cpu_model, "nproc": os.cpu_count(),
+            "runs_tflops": [round(r, 6) for r in runs],
+            "sample": (f"torch fp16 F.linear(x, W_dq) on the host (the reference's eval op, "
+                       f"quant/int_linear.py:62; W_dq from oracle/torch_ref.py), M={M} N={N} "
+                       f"K={K}, {nmat} distinct pre-dequantized int{bits} g{group} matrices, "
+                       f"5 runs of {per_run:.1f}s ({products} products), median; "
+                       f"torch.set_num_threads({threads}) = the CPUs this process may use"),
+            "quantize_every_call_ms": round(statistics.median(calls) * 1e3, 2),
+            "quantize_every_call_calls": len(calls)}
 
 
 def main():

@@ -66,6 +66,16 @@ constexpr int kQKV = 0, kO = 1, kGU = 2, kDN = 3;
 #ifndef DECODE_PF                  // tiles in flight per stream wave (dev knob)
 #define DECODE_PF 16
 #endif
+#ifndef DECODE_TRACE               // dev build: IO-wave event timestamps after the partials
+#define DECODE_TRACE 0
+#endif
+constexpr int kEv = 20;            // trace events per layer
+#ifndef DECODE_POLL_SLEEP          // s_sleep between polls of a cross-CU counter (x 64 clocks):
+#define DECODE_POLL_SLEEP 8        // 256 pollers re-reading counters steal HBM bandwidth
+#endif
+#ifndef DECODE_IO_PRIO             // issue priority of the IO wave over its SIMD's stream wave
+#define DECODE_IO_PRIO 3
+#endif
 #ifndef DECODE_SPIN_LIMIT          // polls before a wait gives up (each ~0.1-1 us)
 #define DECODE_SPIN_LIMIT (1 << 22)
 #endif
@@ -79,6 +89,10 @@ struct Layer {  // == qlin_decode_layer (include/qlin_gfx950.h)
   _Float16* vc;
 };
 static_assert(sizeof(Layer) == 12 * sizeof(void*), "qlin_decode_layer layout");
+static_assert(kMaxGrp * kMaxC >= 1024, "the merge keeps 2 x 512 floats in Smem::pb");
+// the layer table is read-only for the launch: through the constant address space its pointers
+// come by scalar loads (a vector load would make every weight load behind it wait vmcnt(0))
+typedef __attribute__((address_space(4))) const Layer CLayer;
 
 struct Args {
   const Layer* layers;
@@ -104,7 +118,18 @@ struct Args {
   _Float16* gu;
   _Float16* hb;
   float* part;     // attention partials [Hkv][S][grp][kD + 2]
+  unsigned long long* trace;  // DECODE_TRACE: [nl][kEv][ncu] wall_clock64 stamps
 };
+
+// DECODE_TRACE: the IO wave stamps event e of layer l (100 MHz wall clock)
+__device__ __forceinline__ void stamp(const Args& a, int l, int e) {
+  if (DECODE_TRACE && (threadIdx.x & 63) == 0)
+    a.trace[((int64_t)l * kEv + e) * a.ncu + blockIdx.x] = wall_clock64();
+}
+
+__device__ __forceinline__ const CLayer& layer_at(const Args& a, int l) {
+  return ((const CLayer*)(uintptr_t)a.layers)[l];
+}
 
 __device__ __forceinline__ int* cnt_phase(const Args& a, int l, int ph) {
   return a.cnt + 1 + l * a.cnt_stride + ph * kShards;
@@ -178,7 +203,7 @@ __device__ __forceinline__ bool wait_phase(const Args& a, Smem& sm, int l, int p
       return false;
     }
     if (__all(lane >= kShards || v >= want)) return true;
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(DECODE_POLL_SLEEP);
   }
   set_error(a, sm, 3);
   return false;
@@ -194,7 +219,7 @@ __device__ __forceinline__ bool wait_count(const Args& a, Smem& sm, const int* c
       return false;
     }
     if (__builtin_amdgcn_readlane(v, 0) >= want) return true;
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(DECODE_POLL_SLEEP);
   }
   set_error(a, sm, 4);
   return false;
@@ -211,15 +236,40 @@ __device__ __forceinline__ bool wait_done(const Args& a, Smem& sm, int want) {
   return false;
 }
 
-// stream wave: the phase with sequence number `seq` has its input staged
+// stream wave: the phase with sequence number `seq` has its input staged.  The bounded spin is ONE
+// inline-asm block: a loop in the compiler's CFG inside the unrolled tile body makes hipcc's
+// waitcnt pass give up its per-slot counts and drain the whole prefetch (vmcnt(0)) every tile
 __device__ __forceinline__ bool wait_ready(Smem& sm, int seq) {
-  for (int spin = 0; spin < DECODE_SPIN_LIMIT; ++spin) {
-    if (__hip_atomic_load(&sm.xready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= seq)
-      return true;
-    if (__hip_atomic_load(&sm.abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return false;
+  typedef __attribute__((address_space(3))) int lds_int;
+  const uint32_t xa = (uint32_t)(uintptr_t)(lds_int*)&sm.xready;
+  const uint32_t aa = (uint32_t)(uintptr_t)(lds_int*)&sm.abort_;
+  int ok, sv, cnt, v, w;
+  asm volatile(
+      "s_mov_b32 %[cnt], %[lim]\n"
+      "1:\n\t"
+      "ds_read_b32 %[v], %[xa]\n\t"
+      "ds_read_b32 %[w], %[aa]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %[sv], %[v]\n\t"
+      "s_cmp_ge_i32 %[sv], %[seq]\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "v_readfirstlane_b32 %[sv], %[w]\n\t"
+      "s_cmp_lg_u32 %[sv], 0\n\t"
+      "s_cbranch_scc1 3f\n\t"
+      "s_sleep 2\n\t"
+      "s_sub_u32 %[cnt], %[cnt], 1\n\t"
+      "s_cmp_lg_u32 %[cnt], 0\n\t"
+      "s_cbranch_scc1 1b\n"
+      "3:\n\t"
+      "s_mov_b32 %[ok], 0\n\t"
+      "s_branch 4f\n"
+      "2:\n\t"
+      "s_mov_b32 %[ok], 1\n"
+      "4:"
+      : [ok] "=s"(ok), [sv] "=&s"(sv), [cnt] "=&s"(cnt), [v] "=&v"(v), [w] "=&v"(w)
+      : [xa] "v"(xa), [aa] "v"(aa), [seq] "s"(seq), [lim] "s"(DECODE_SPIN_LIMIT)
+      : "memory", "scc");
+  return ok != 0;
 }
 
 __device__ __forceinline__ int seq_of(int l, int ph) { return l * kPhases + ph + 1; }
@@ -227,47 +277,74 @@ __device__ __forceinline__ int seq_of(int l, int ph) { return l * kPhases + ph +
 // ---------------------------------------------------------------------------------------------
 // IO wave helpers
 // ---------------------------------------------------------------------------------------------
-// n halfs (n % 4 == 0) from global into LDS; sc1: written earlier in this launch by other CUs
-__device__ __forceinline__ void stage(_Float16* dst, const _Float16* src, int n, bool sc1) {
+// n halfs from global into LDS by LDS-DMA: every 1-KB piece in flight at once, one wait (the
+// IO wave otherwise pays one memory round trip per batch of loads).  SC1: the vector was written
+// earlier in this launch by other CUs (write-through) — the loads bypass this CU's L1.  The last
+// piece may run past n: its lanes re-read the vector's last 16 B into the buffer's padding (every
+// LDS vector buffer is a multiple of 1 KB)
+template <bool SC1>
+__device__ __forceinline__ void stage(_Float16* dst, const _Float16* src, int n) {
   const int lane = threadIdx.x & 63;
-  const int n4 = n >> 2;
-  unsigned long long* d = reinterpret_cast<unsigned long long*>(dst);
-  const unsigned long long* s = reinterpret_cast<const unsigned long long*>(src);
-  for (int b = 0; b < n4; b += 64 * 8) {
-    unsigned long long v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int i = min(b + 64 * k + lane, n4 - 1);
-      v[k] = sc1 ? ld_sc1_64(s + i) : s[i];
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int i = b + 64 * k + lane;
-      if (i < n4) d[i] = v[k];
-    }
+  const int nb = n * 2;
+  const unsigned char* s = reinterpret_cast<const unsigned char*>(src);
+  unsigned char* d = reinterpret_cast<unsigned char*>(dst);
+  for (int i = 0; i * 1024 < nb; ++i) {
+    const int off = min(i * 1024 + lane * 16, nb - 16);
+    __builtin_amdgcn_global_load_lds((gbl_ptr)(s + off), (lds_ptr)(d + i * 1024), 16, 0,
+                                     SC1 ? 16 : 0);
   }
+  drain();
 }
 
 // RMSNorm (OmniLlamaRMSNorm, quant/omni_norm.py:52-63 of the reference; the fused norm of
-// qlin_rmsnorm_linear_ep): dst = RN16(w * (x * rsqrt(mean(x^2) + eps))), the sum of squares in a
-// fixed lane-strided + butterfly order, so every CU forms the same normed vector
-__device__ __forceinline__ void rmsnorm_lds(_Float16* dst, const _Float16* x, const float* w, int H, float eps) {
+// qlin_rmsnorm_linear_ep), fused with the staging of its input: x (H halfs) arrives in `res` by
+// LDS-DMA while the norm weights come into registers (32 per lane per round: one memory round
+// trip for H <= 4096 instead of one per element group), then dst = RN16(w * (x * rsqrt(mean(x^2)
+// + eps))) with the sum of squares in a fixed lane-strided + butterfly order, so every CU forms
+// the same normed vector
+template <bool SC1>
+__device__ __forceinline__ void stage_norm(_Float16* res, _Float16* dst, const _Float16* src,
+                                           const float* w, int H, float eps) {
 #pragma clang fp contract(off)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(1))) const f2v gf2;
   const int lane = threadIdx.x & 63;
+  const int nb = H * 2;
+  const unsigned char* s = reinterpret_cast<const unsigned char*>(src);
+  unsigned char* d = reinterpret_cast<unsigned char*>(res);
+  for (int i = 0; i * 1024 < nb; ++i) {
+    const int off = min(i * 1024 + lane * 16, nb - 16);
+    __builtin_amdgcn_global_load_lds((gbl_ptr)(s + off), (lds_ptr)(d + i * 1024), 16, 0,
+                                     SC1 ? 16 : 0);
+  }
+  constexpr int R = 32;  // float2 weight loads per lane per round
+  f2v ww[R];
+  auto load_w = [&](int k0) {
+#pragma unroll
+    for (int c = 0; c < R; ++c) ww[c] = *((gf2*)(w + min(k0 + 128 * c + 2 * lane, H - 2)));
+  };
+  load_w(0);
+  drain();
   float ss = 0.f;
   for (int k = 2 * lane; k < H; k += 128) {
-    const h2 v = *reinterpret_cast<const h2*>(x + k);
+    const h2 v = *reinterpret_cast<const h2*>(res + k);
     const float f0 = (float)v.x, f1 = (float)v.y;
     ss = ss + f0 * f0;
     ss = ss + f1 * f1;
   }
   ss = wave_sum(ss);
   const float rn = rsqrtf(ss / (float)H + eps);
-  for (int k = 2 * lane; k < H; k += 128) {
-    const h2 v = *reinterpret_cast<const h2*>(x + k);
-    const float2 ww = *reinterpret_cast<const float2*>(w + k);
-    const float n0 = ww.x * ((float)v.x * rn), n1 = ww.y * ((float)v.y * rn);
-    *reinterpret_cast<h2*>(dst + k) = h2{(_Float16)n0, (_Float16)n1};
+  for (int k0 = 0; k0 < H; k0 += 128 * R) {
+    if (k0) load_w(k0);
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const int k = k0 + 128 * c + 2 * lane;
+      if (k < H) {
+        const h2 v = *reinterpret_cast<const h2*>(res + k);
+        const float n0 = ww[c].x * ((float)v.x * rn), n1 = ww[c].y * ((float)v.y * rn);
+        *reinterpret_cast<h2*>(dst + k) = h2{(_Float16)n0, (_Float16)n1};
+      }
+    }
   }
 }
 
@@ -302,7 +379,7 @@ __device__ __forceinline__ int unit_cu(int u, int U, int G) { return (int)(((int
 __device__ __forceinline__ int kv_off(int t, int seg) { return t * kD + ((seg ^ (t & 15)) << 3); }
 
 // LDS-DMA the chunk's cached rows (rows < L0) of layer l, head g
-__device__ __forceinline__ void prefetch_kv(const Args& a, Smem& sm, const Layer& ly, int g, int ch) {
+__device__ __forceinline__ void prefetch_kv(const Args& a, Smem& sm, const CLayer& ly, int g, int ch) {
   const int lane = threadIdx.x & 63;
   const int t0 = ch * a.C;
   const int n = min(a.C, a.L0 - t0);  // cached rows in the chunk (the new row comes later)
@@ -332,7 +409,7 @@ __device__ __forceinline__ float h2f_hi(uint32_t w) {
 __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u, bool prefetched) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
-  const Layer& ly = a.layers[l];
+  const CLayer& ly = layer_at(a, l);
   const int S = a.S, C = a.C, grp = a.grp;
   const int g = u / S, ch = u - g * S;
   const int L = a.L0 + 1;
@@ -345,21 +422,31 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
   const float* sr = a.sinc + p * kD;
   const float c0 = (float)(_Float16)cr[lane], c1 = (float)(_Float16)cr[lane + 64];
   const float s0 = (float)(_Float16)sr[lane], s1 = (float)(_Float16)sr[lane + 64];
-  for (int h = 0; h < grp; ++h) {
-    const _Float16* q = a.qkv + (int64_t)(g * grp + h) * kD;
-    const uint32_t w0 = ld_sc1(q + (lane & ~1)), w1 = ld_sc1(q + 64 + (lane & ~1));
-    const float x0 = (lane & 1) ? h2f_hi(w0) : h2f_lo(w0);
-    const float x1 = (lane & 1) ? h2f_hi(w1) : h2f_lo(w1);
-    // rotate_half: out[d] = x[d] c[d] - x[d + 64] s[d]; out[d + 64] = x[d + 64] c[d + 64] + x[d] s[d + 64]
-    sm.qs[h][lane] = x0 * c0 + (-x1) * s0;
-    sm.qs[h][lane + 64] = x1 * c1 + x0 * s1;
+  // every q / k / v word of the unit issued at once (one round trip), then RoPE
+  uint32_t qw0[kMaxGrp], qw1[kMaxGrp];
+#pragma unroll
+  for (int h = 0; h < kMaxGrp; ++h) {
+    const _Float16* q = a.qkv + (int64_t)(g * grp + min(h, grp - 1)) * kD;
+    qw0[h] = ld_sc1(q + (lane & ~1));
+    qw1[h] = ld_sc1(q + 64 + (lane & ~1));
   }
+  const _Float16* kp = a.qkv + a.H + (int64_t)g * kD;
+  const _Float16* vp = a.qkv + a.H + a.Hkv * kD + (int64_t)g * kD;
+  const uint32_t k0w = ld_sc1(kp + (lane & ~1)), k1w = ld_sc1(kp + 64 + (lane & ~1));
+  const uint32_t v0w = ld_sc1(vp + (lane & ~1)), v1w = ld_sc1(vp + 64 + (lane & ~1));
+#pragma unroll
+  for (int h = 0; h < kMaxGrp; ++h) {
+    if (h < grp) {
+      const float x0 = (lane & 1) ? h2f_hi(qw0[h]) : h2f_lo(qw0[h]);
+      const float x1 = (lane & 1) ? h2f_hi(qw1[h]) : h2f_lo(qw1[h]);
+      // rotate_half: out[d] = x[d] c[d] - x[d + 64] s[d]; out[d + 64] = x[d + 64] c[d + 64] + x[d] s[d + 64]
+      sm.qs[h][lane] = x0 * c0 + (-x1) * s0;
+      sm.qs[h][lane + 64] = x1 * c1 + x0 * s1;
+    }
+  }
+  stamp(a, l, 14);
   const bool has_new = t0 + n == L;  // this chunk holds the new row L0
   if (has_new) {
-    const _Float16* k = a.qkv + a.H + (int64_t)g * kD;
-    const _Float16* v = a.qkv + a.H + a.Hkv * kD + (int64_t)g * kD;
-    const uint32_t k0w = ld_sc1(k + (lane & ~1)), k1w = ld_sc1(k + 64 + (lane & ~1));
-    const uint32_t v0w = ld_sc1(v + (lane & ~1)), v1w = ld_sc1(v + 64 + (lane & ~1));
     const float x0 = (lane & 1) ? h2f_hi(k0w) : h2f_lo(k0w);
     const float x1 = (lane & 1) ? h2f_hi(k1w) : h2f_lo(k1w);
     // fp16 ops, as the reference's k path (fp16 cos / sin)
@@ -390,6 +477,7 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
     }
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes visible to this wave's reads
+  stamp(a, l, 15);
   // scores: lane = row t (and t + 64 for 128-row chunks); fp32 dot products over the 128 dims
   float mloc[kMaxGrp];
 #pragma unroll
@@ -434,6 +522,7 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
       }
     }
   }
+  stamp(a, l, 16);
   float m[kMaxGrp], lsum[kMaxGrp];
 #pragma unroll
   for (int h = 0; h < kMaxGrp; ++h) {
@@ -454,6 +543,7 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
       lsum[h] = s_;
     }
   }
+  stamp(a, l, 17);
   // P V: lane owns dims 2 * lane, 2 * lane + 1 (segment lane / 4 of each row)
   float o0[kMaxGrp], o1[kMaxGrp];
 #pragma unroll
@@ -471,6 +561,7 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
       }
     }
   }
+  stamp(a, l, 18);
   const int64_t qh0 = (int64_t)g * grp;  // first query head of the group
   if (S == 1) {
 #pragma unroll
@@ -502,29 +593,65 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
   int old = 0;
   if (lane == 0) old = add_agent(cnt_head(a, l, g), 1);
   old = __builtin_amdgcn_readfirstlane(old);
+  stamp(a, l, 19);
   if (old != S - 1) return true;
-  // merge: weights exp(m_s - M), denominators sum_s w_s l_s (qlin_attn_decode's merge)
+  // merge (qlin_attn_decode's): weights w_s = exp(m_s - M), denominators sum_s w_s l_s.  The
+  // (m, l) of all S x grp partials arrive in one round of 8-B loads (lane j: partial j), the
+  // weights go through LDS (sm.pb), then the partial rows in rounds of <= 32 8-B loads per lane
   const float* pg = a.part + (int64_t)g * S * grp * (kD + 2);
-  for (int h = 0; h < grp; ++h) {
-    float M = -INFINITY;
-    for (int s = lane; s < S; s += 64)
-      M = fmaxf(M, __builtin_bit_cast(float, ld_sc1(pg + ((int64_t)s * grp + h) * (kD + 2) + kD)));
-    for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
-    float den = 0.f;
-    for (int s = lane; s < S; s += 64) {
-      const float* ps = pg + ((int64_t)s * grp + h) * (kD + 2);
-      const float w = expf(__builtin_bit_cast(float, ld_sc1(ps + kD)) - M);
-      den += w * __builtin_bit_cast(float, ld_sc1(ps + kD + 1));
+  const int np = S * grp;  // partial j = s * grp + h (<= 512: S <= 64, grp <= 8)
+  float* pbf = &sm.pb[0][0];  // m (then the weight) of partial j at pbf[j], l at pbf[512 + j]
+  for (int j0 = 0; j0 < np; j0 += 64) {
+    const int j = min(j0 + lane, np - 1);
+    const unsigned long long ml = ld_sc1_64(pg + (int64_t)j * (kD + 2) + kD);
+    if (j0 + lane < np) {
+      pbf[j0 + lane] = __builtin_bit_cast(float, (uint32_t)ml);
+      pbf[512 + j0 + lane] = __builtin_bit_cast(float, (uint32_t)(ml >> 32));
     }
-    for (int o = 32; o > 0; o >>= 1) den += __shfl_xor(den, o);
-    float a0 = 0.f, a1 = 0.f;
-    for (int s = 0; s < S; ++s) {
-      const float* ps = pg + ((int64_t)s * grp + h) * (kD + 2);
-      const float w = expf(__builtin_bit_cast(float, ld_sc1(ps + kD)) - M);
-      a0 = fmaf(w, __builtin_bit_cast(float, ld_sc1(ps + 2 * lane)), a0);
-      a1 = fmaf(w, __builtin_bit_cast(float, ld_sc1(ps + 2 * lane + 1)), a1);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  float den[kMaxGrp], acc0[kMaxGrp], acc1[kMaxGrp];
+#pragma unroll
+  for (int h = 0; h < kMaxGrp; ++h) {
+    den[h] = acc0[h] = acc1[h] = 0.f;
+    if (h < grp) {
+      float M = -INFINITY;
+      for (int s_ = 0; s_ < S; ++s_) M = fmaxf(M, pbf[s_ * grp + h]);
+      for (int s_ = 0; s_ < S; ++s_) {
+        const float w = expf(pbf[s_ * grp + h] - M);
+        den[h] += w * pbf[512 + s_ * grp + h];
+        pbf[s_ * grp + h] = w;
+      }
     }
-    const _Float16 r0 = (_Float16)(a0 / den), r1 = (_Float16)(a1 / den);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  const int SR = 32 / grp;  // partial rows (s values) per round: <= 32 8-B loads per lane
+  for (int s0 = 0; s0 < S; s0 += SR) {
+    unsigned long long ov[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int s_ = min(s0 + k / grp, S - 1), h = k % grp;
+      ov[k] = ld_sc1_64(pg + ((int64_t)s_ * grp + h) * (kD + 2) + 2 * lane);
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int s_ = s0 + k / grp, h = k % grp;
+      if (s_ < S) {
+#pragma unroll
+        for (int hh = 0; hh < kMaxGrp; ++hh) {
+          if (hh == h) {
+            const float w = pbf[s_ * grp + hh];
+            acc0[hh] = fmaf(w, __builtin_bit_cast(float, (uint32_t)ov[k]), acc0[hh]);
+            acc1[hh] = fmaf(w, __builtin_bit_cast(float, (uint32_t)(ov[k] >> 32)), acc1[hh]);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < kMaxGrp; ++h) {
+    if (h >= grp) break;
+    const _Float16 r0 = (_Float16)(acc0[h] / den[h]), r1 = (_Float16)(acc1[h] / den[h]);
     st_sc1(a.abuf + (qh0 + h) * kD + 2 * lane,
            (uint32_t)__builtin_bit_cast(uint16_t, r0) |
                ((uint32_t)__builtin_bit_cast(uint16_t, r1) << 16));
@@ -539,46 +666,58 @@ __device__ __forceinline__ void io_wave(const Args& a, Smem& sm) {
   const int U = a.Hkv * a.S;
   int done_total = 0;
   for (int l = 0; l < a.nl; ++l) {
-    const Layer& ly = a.layers[l];
+    const CLayer& ly = layer_at(a, l);
+    stamp(a, l, 0);
     // --- q/k/v: the layer input h (launch input, or the previous layer's down output) + norm
     if (l == 0) {
-      stage(sm.hres, a.x, a.H, false);
+      stage_norm<false>(sm.hres, sm.xbuf, a.x, ly.w_in, a.H, a.eps);
     } else {
       if (!wait_phase(a, sm, l - 1, kDN)) return;
-      stage(sm.hres, a.hb, a.H, true);
+      stage_norm<true>(sm.hres, sm.xbuf, a.hb, ly.w_in, a.H, a.eps);
     }
-    rmsnorm_lds(sm.xbuf, sm.hres, ly.w_in, a.H, a.eps);
     __hip_atomic_store(&sm.xready, seq_of(l, kQKV), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    stamp(a, l, 1);
     // this CU's first attention unit of the layer: its cached K / V rows, early
     int u0 = -1;
     for (int u = 0; u < U; ++u)
       if (unit_cu(u, U, a.ncu) == c) { u0 = u; break; }
     if (u0 >= 0) prefetch_kv(a, sm, ly, u0 / a.S, u0 % a.S);
     if (!publish(a, sm, l, kQKV, done_total)) return;
+    stamp(a, l, 2);
     // --- attention units of this CU
     if (u0 >= 0) {
       if (!wait_phase(a, sm, l, kQKV)) return;
+      stamp(a, l, 3);
       for (int u = u0; u < U; ++u) {
         if (unit_cu(u, U, a.ncu) != c) continue;
         if (!attn_unit(a, sm, l, u, u == u0)) return;
       }
+      stamp(a, l, 4);
     }
     // --- o_proj (+ residual h)
     if (!wait_count(a, sm, cnt_attn(a, l), a.Hkv)) return;
-    stage(sm.xbuf, a.abuf, a.H, true);
+    stamp(a, l, 5);
+    stage<true>(sm.xbuf, a.abuf, a.H);
     __hip_atomic_store(&sm.xready, seq_of(l, kO), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    stamp(a, l, 6);
     if (!publish(a, sm, l, kO, done_total)) return;
+    stamp(a, l, 7);
     // --- gate/up (+ norm, SiLU * up)
     if (!wait_phase(a, sm, l, kO)) return;
-    stage(sm.h2res, a.h2, a.H, true);
-    rmsnorm_lds(sm.xbuf, sm.h2res, ly.w_post, a.H, a.eps);
+    stamp(a, l, 8);
+    stage_norm<true>(sm.h2res, sm.xbuf, a.h2, ly.w_post, a.H, a.eps);
     __hip_atomic_store(&sm.xready, seq_of(l, kGU), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    stamp(a, l, 9);
     if (!publish(a, sm, l, kGU, done_total)) return;
+    stamp(a, l, 10);
     // --- down (+ residual h2)
     if (!wait_phase(a, sm, l, kGU)) return;
-    stage(sm.xbuf, a.gu, a.I, true);
+    stamp(a, l, 11);
+    stage<true>(sm.xbuf, a.gu, a.I);
     __hip_atomic_store(&sm.xready, seq_of(l, kDN), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    stamp(a, l, 12);
     if (!publish(a, sm, l, kDN, done_total)) return;
+    stamp(a, l, 13);
   }
 }
 
@@ -588,7 +727,10 @@ __device__ __forceinline__ void io_wave(const Args& a, Smem& sm) {
 // a wave's position in its tile sequence: layer, phase, flat index t of the CU's phase tiles
 // (row-major over its rows), end of the wave's run in this phase
 struct Cur {
-  int l, ph, t, tend, T, i, kt;
+  int l, ph, t, tend, T, i, kt, Kt, Gs;
+  const gu32* qw;  // this run's phase matrix (uniform)
+  const gu32* sz;
+  bool done;       // load cursor past the wave's last tile: it repeats that tile
 };
 
 __device__ __forceinline__ void run_of(const Args& a, int ph, int wave, int& t, int& tend, int& T) {
@@ -598,7 +740,8 @@ __device__ __forceinline__ void run_of(const Args& a, int ph, int wave, int& t, 
   tend = (int)(((int64_t)(wave + 1) * T) / kStream);
 }
 
-// move to the first tile of the next non-empty run (or l == nl: the end)
+// the next non-empty run after (c.l, c.ph), or c.l == nl at the end; the run's operands come from
+// the layer table through the constant address space (scalar loads: no vmcnt wait in the stream)
 __device__ __forceinline__ void next_run(const Args& a, Cur& c, int wave) {
   for (;;) {
     if (++c.ph == kPhases) {
@@ -608,32 +751,29 @@ __device__ __forceinline__ void next_run(const Args& a, Cur& c, int wave) {
     run_of(a, c.ph, wave, c.t, c.tend, c.T);
     if (c.t < c.tend) break;
   }
-  c.i = c.t / a.Kt[c.ph];
-  c.kt = c.t - c.i * a.Kt[c.ph];
+  c.Kt = a.Kt[c.ph];
+  c.Gs = a.Gs[c.ph];
+  c.i = c.t / c.Kt;
+  c.kt = c.t - c.i * c.Kt;
+  const CLayer& ly = layer_at(a, c.l);
+  c.qw = (const gu32*)ly.qw[c.ph];
+  c.sz = (const gu32*)ly.sz[c.ph];
 }
 
-__device__ __forceinline__ void first_run(const Args& a, Cur& c, int wave) {
-  c.l = 0;
-  c.ph = -1;
-  c.t = c.tend = 0;
-  // phase -1 + 1 = 0 of layer 0
-  for (;;) {
-    if (++c.ph == kPhases) {
-      c.ph = 0;
-      if (++c.l == a.nl) return;
-    }
-    run_of(a, c.ph, wave, c.t, c.tend, c.T);
-    if (c.t < c.tend) break;
-  }
-  c.i = c.t / a.Kt[c.ph];
-  c.kt = c.t - c.i * a.Kt[c.ph];
-}
-
-// advance one tile; true when the tile just passed ended an item (a row or the run)
+// advance one tile; true when the tile just passed ended an item (a row or the run).  Past the
+// wave's last tile the load cursor stays on its last row (done), so every slot is loaded
+// unconditionally
 __device__ __forceinline__ bool advance(const Args& a, Cur& c, int wave) {
+  if (c.done) {
+    // keep loading valid tiles of the last row, each at a new address: a load the compiler can
+    // prove equal to the previous one is replaced by a copy of its result (a vmcnt(0) wait)
+    c.kt = c.kt + 1 == c.Kt ? 0 : c.kt + 1;
+    return false;
+  }
+  const Cur prev = c;
   ++c.t;
   bool end = false;
-  if (++c.kt == a.Kt[c.ph]) {
+  if (++c.kt == c.Kt) {
     c.kt = 0;
     ++c.i;
     end = true;
@@ -641,8 +781,39 @@ __device__ __forceinline__ bool advance(const Args& a, Cur& c, int wave) {
   if (c.t == c.tend) {
     next_run(a, c, wave);
     end = true;
+    if (c.l == a.nl) {
+      c = prev;
+      c.done = true;
+    }
   }
   return end;
+}
+
+template <int BITS>
+__device__ __forceinline__ Piece<BITS> load_piece_g(const gu32* p) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+  typedef __attribute__((address_space(1))) const u32x4 g4;
+  typedef __attribute__((address_space(1))) const u32x2 g2;
+  typedef __attribute__((address_space(1))) const u32x3 g3;
+  Piece<BITS> c;
+  if constexpr (BITS == 4) {
+    const u32x4 v = __builtin_nontemporal_load((g4*)p);
+    c.w[0] = v.x; c.w[1] = v.y; c.w[2] = v.z; c.w[3] = v.w;
+  } else if constexpr (BITS == 8) {
+    const u32x4 v0 = __builtin_nontemporal_load((g4*)p);
+    const u32x4 v1 = __builtin_nontemporal_load((g4*)(p + 4));
+    c.w[0] = v0.x; c.w[1] = v0.y; c.w[2] = v0.z; c.w[3] = v0.w;
+    c.w[4] = v1.x; c.w[5] = v1.y; c.w[6] = v1.z; c.w[7] = v1.w;
+  } else if constexpr (BITS == 2) {
+    const u32x2 v = __builtin_nontemporal_load((g2*)p);
+    c.w[0] = v.x; c.w[1] = v.y;
+  } else {
+    const u32x3 v = __builtin_nontemporal_load((g3*)p);
+    c.w[0] = v.x; c.w[1] = v.y; c.w[2] = v.z;
+  }
+  return c;
 }
 
 template <int BITS, int GPT, int ZM, int PF>
@@ -658,33 +829,33 @@ __device__ __forceinline__ void stream_wave(const Args& a, Smem& sm, int wave) {
   total *= a.nl;
   if (total == 0) return;
 
-  Cur lc, cc;
-  first_run(a, lc, wave);
-  cc = lc;
+  Cur lc;
+  lc.l = 0;
+  lc.ph = -1;
+  lc.done = false;
+  next_run(a, lc, wave);  // total > 0: a run exists
+  Cur cc = lc;
   auto group_of_tile = [&](int kt) {
     return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
   };
   WTile<BITS, GPT> wt[PF];
   auto load = [&](int u) {
-    const Layer& ly = a.layers[lc.l];
-    const int ph = lc.ph;
-    const int r = cu + lc.i * a.ncu;  // global tile row
-    const uint32_t* qw = ly.qw[ph] + ((int64_t)r * a.Kt[ph] + lc.kt) * (64 * BITS) + lane * BITS;
-    wt[u].pc = load_piece_nt<BITS>(qw);
-    const uint32_t* sz = ly.sz[ph] + (int64_t)r * a.Gs[ph] * kTileN + n_in;
+    const int64_t r = cu + lc.i * a.ncu;  // global tile row
+    wt[u].pc = load_piece_g<BITS>(lc.qw + (r * lc.Kt + lc.kt) * (64 * BITS) + lane * BITS);
+    const gu32* sz = lc.sz + r * lc.Gs * kTileN + n_in;
     const int g0 = group_of_tile(lc.kt);
 #pragma unroll
     for (int s = 0; s < GPT; ++s) wt[u].sz[s] = sz[(g0 + s) * kTileN];
+    advance(a, lc, wave);
   };
 
   const Magics mg = make_magics<BITS>();
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   int ready = 0;  // highest phase sequence known staged
 
-  // flush the item the compute cursor just finished (row i of phase ph, layer l): lanes 0..15
-  // hold the row's 16 (partial) outputs in acc[0]
-  auto flush = [&](int l, int ph, int i, int T) {
-    const int Kt = a.Kt[ph];
+  // flush the item the compute cursor just finished (row i of phase ph): lanes 0..15 hold the
+  // row's 16 (partial) outputs in acc[0]
+  auto flush = [&](int ph, int i, int T, int Kt) {
     const int lo = i * Kt, hi = lo + Kt;
     int nsplit = 0, j = 0;
     for (int w = 0; w < kStream; ++w) {
@@ -712,7 +883,7 @@ __device__ __forceinline__ void stream_wave(const Args& a, Smem& sm, int wave) {
     const int r = cu + i * a.ncu;
     const float t16 = (float)(_Float16)v;  // F.linear's fp16 output
     if (ph == kGU) {
-      // interleaved gate rows 8r'.. (lanes 0-7) and up rows (lanes 8-15): silu(gate) * up
+      // interleaved gate rows (lanes 0-7) and up rows (lanes 8-15): silu(gate) * up
       const float up = __shfl(t16, (lane & 7) + 8);
       if (lane < 8) sm.ostage[i][lane] = (_Float16)(silu_rn16(t16) * up);
     } else if (lane < kTileN) {
@@ -721,13 +892,17 @@ __device__ __forceinline__ void stream_wave(const Args& a, Smem& sm, int wave) {
       if (ph == kDN) o = (float)sm.h2res[r * kTileN + lane] + t16;
       sm.ostage[i][lane] = (_Float16)o;
     }
-    if (lane == 0) __hip_atomic_fetch_add(&sm.ndone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0)
+      __hip_atomic_fetch_add(&sm.ndone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
 
-  auto compute = [&](int u) -> bool {
+  // compute slot u (the compute cursor's tile).  After an abort (a timed-out wait anywhere) the
+  // waits return at once and the wave runs out its (valid, bounded) tile sequence on garbage: an
+  // early exit from this loop makes hipcc drain vmcnt at every tile
+  auto compute = [&](int u) {
     const int seq = seq_of(cc.l, cc.ph);
-    if (seq > ready) {
-      if (!wait_ready(sm, seq)) return false;
+    if (__builtin_expect(seq > ready, 0)) {
+      wait_ready(sm, seq);
       ready = seq;
     }
     const _Float16* xb = sm.xbuf + cc.kt * kTileK + 8 * q;
@@ -746,31 +921,22 @@ __device__ __forceinline__ void stream_wave(const Args& a, Smem& sm, int wave) {
     step(std::integral_constant<int, 1>{});
     step(std::integral_constant<int, 2>{});
     step(std::integral_constant<int, 3>{});
-    const int l = cc.l, ph = cc.ph, i = cc.i, T = cc.T;
-    if (advance(a, cc, wave)) {
-      flush(l, ph, i, T);
+    const int ph = cc.ph, i = cc.i, T = cc.T, Kt = cc.Kt;
+    if (__builtin_expect(advance(a, cc, wave), 0)) {
+      flush(ph, i, T, Kt);
       acc = f4{0.f, 0.f, 0.f, 0.f};
     }
-    return true;
   };
 
+  // every slot is loaded unconditionally (the load cursor repeats the wave's last tile once it is
+  // past it), so hipcc counts the loads with vmcnt(N) instead of draining at each branch
 #pragma unroll
-  for (int u = 0; u < PF; ++u) {
-    if (u < total) {
-      load(u);
-      advance(a, lc, wave);
-    }
-  }
+  for (int u = 0; u < PF; ++u) load(u);
   for (int base = 0; base < total; base += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
-      if (base + u < total) {
-        if (!compute(u)) return;
-        if (base + u + PF < total) {
-          load(u);
-          advance(a, lc, wave);
-        }
-      }
+      if (base + u < total) compute(u);
+      load(u);
     }
   }
 }
@@ -786,7 +952,12 @@ __global__ __launch_bounds__(64 * kWaves) void decode_kernel(const Args a) {
   }
   if (threadIdx.x < kMaxRows) sm.rowcnt[threadIdx.x] = 0;
   __syncthreads();
-  if (wave == 0) io_wave(a, sm);
+  if (wave == 0) {
+    // the IO wave's serial work (staging, norms, attention, publishing) is every CU's critical
+    // path; the stream wave sharing its SIMD yields issue slots to it
+    __builtin_amdgcn_s_setprio(DECODE_IO_PRIO);
+    io_wave(a, sm);
+  }
   else stream_wave<BITS, GPT, ZM, DECODE_PF>(a, sm, wave - 1);
 }
 
@@ -800,7 +971,7 @@ struct Dims {
 int64_t cnt_stride_of(const Dims& d) { return kPhases * kShards + 1 + d.Hkv; }
 
 struct WsLayout {
-  int64_t cnt_bytes, qkv, abuf, h2, gu, hb, part, total;
+  int64_t cnt_bytes, qkv, abuf, h2, gu, hb, part, trace, total;
 };
 
 int64_t up256(int64_t v) { return (v + 255) / 256 * 256; }
@@ -816,7 +987,8 @@ WsLayout ws_layout(const Dims& d, int64_t max_L) {
   w.gu = w.h2 + up256(d.H * 2);
   w.hb = w.gu + up256(d.I * 2);
   w.part = w.hb + up256(d.H * 2);
-  w.total = w.part + up256((int64_t)d.Hkv * Smax * grp * (kD + 2) * 4);
+  w.trace = w.part + up256((int64_t)d.Hkv * Smax * grp * (kD + 2) * 4);
+  w.total = w.trace + (DECODE_TRACE ? up256((int64_t)d.nl * kEv * cu_count_cached() * 8) : 0);
   return w;
 }
 
@@ -861,7 +1033,7 @@ extern "C" int qlin_decode_llama_f16(const void* layers, int n_layers, int64_t H
   if (!layers || !x || !y || !cos_cache || !sin_cache || !position || !workspace ||
       !qlin_decode_supported(n_layers, H, I, Hq, Hkv, D, bits, group, flags) || L0 < 0 ||
       L0 + 1 > kMaxL || kv_rows < L0 + 1 || cache_rows < 1 || !(eps >= 0.f) ||
-      !(scale_div > 0.f) || ((uintptr_t)x & 7) || ((uintptr_t)y & 3))
+      !(scale_div > 0.f) || ((uintptr_t)x & 15) || ((uintptr_t)y & 3))
     return QLIN_EINVAL;
   const WsLayout w = ws_layout(d, L0 + 1);
   if (workspace_bytes < w.total || ((uintptr_t)workspace & 255)) return QLIN_EINVAL;
@@ -910,6 +1082,7 @@ extern "C" int qlin_decode_llama_f16(const void* layers, int n_layers, int64_t H
   a.gu = (_Float16*)(ws + w.gu);
   a.hb = (_Float16*)(ws + w.hb);
   a.part = (float*)(ws + w.part);
+  a.trace = (unsigned long long*)(ws + w.trace);
   hipError_t e = hipMemsetAsync(ws, 0, (size_t)w.cnt_bytes, st);
   if (e != hipSuccess) return (int)e;
   const int zm = zero_mode(flags);

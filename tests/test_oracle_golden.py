@@ -194,3 +194,23 @@ def test_quant_matmul_act_quant():
     a, *_ = O.quantize(g["x1"], 8, None)
     b, *_ = O.quantize(g["x2"], 8, None)
     np.testing.assert_allclose(a @ b, g["y_a8"], rtol=1e-5, atol=1e-5)
+
+
+TORCH_REF_CASES = ["q_w4g128_f16", "q_w3g64_f16", "q_w2g64_f16", "q_w8pc_f16", "q_w4pc_f16_k4096",
+                   "q_w4g128_sym_f16", "q_w4g128_nozp_f16", "q_w8g128_nozp_f16", "q_w4g128_f32"]
+
+
+@pytest.mark.parametrize("name", TORCH_REF_CASES)
+def test_torch_cpu_restatement_bit_exact(name):
+    """oracle/torch_ref.py (the bench's CPU baseline: the reference's fake-quant op sequence in
+    torch on the host) reproduces the reference's W_dq / scale / zp bit for bit."""
+    import torch
+    from oracle import torch_ref as TR
+    g = load_golden(name)
+    p = params(g)
+    w_dq, scale, zp = TR.quantize(torch.from_numpy(g["w"]), p["n_bits"], p["group_size"],
+                                  p["symmetric"], p["disable_zero_point"])
+    assert bit_equal(w_dq.numpy(), g["w_dq"]), name
+    assert bit_equal(scale.numpy().reshape(g["scale"].shape), g["scale"]), name
+    if "zp" in g and zp is not None:
+        assert bit_equal(zp.numpy().reshape(g["zp"].shape), g["zp"]), name
