@@ -69,12 +69,15 @@ constexpr int kQKV = 0, kO = 1, kGU = 2, kDN = 3;
 #ifndef DECODE_TRACE               // dev build: IO-wave event timestamps after the partials
 #define DECODE_TRACE 0
 #endif
-constexpr int kEv = 20;            // trace events per layer
+constexpr int kEv = 28;            // trace events per layer
 #ifndef DECODE_POLL_SLEEP          // s_sleep between polls of a cross-CU counter (x 64 clocks):
 #define DECODE_POLL_SLEEP 8        // 256 pollers re-reading counters steal HBM bandwidth
 #endif
 #ifndef DECODE_IO_PRIO             // issue priority of the IO wave over its SIMD's stream wave
 #define DECODE_IO_PRIO 3
+#endif
+#ifndef DECODE_STREAM_ONLY         // dev ablation (wrong results): every phase input "ready" at
+#define DECODE_STREAM_ONLY 0       // once, no IO work: the stream waves' weight throughput alone
 #endif
 #ifndef DECODE_SPIN_LIMIT          // polls before a wait gives up (each ~0.1-1 us)
 #define DECODE_SPIN_LIMIT (1 << 22)
@@ -121,7 +124,8 @@ struct Args {
   unsigned long long* trace;  // DECODE_TRACE: [nl][kEv][ncu] wall_clock64 stamps
 };
 
-// DECODE_TRACE: the IO wave stamps event e of layer l (100 MHz wall clock)
+// DECODE_TRACE: the IO wave stamps event e of layer l (100 MHz wall clock); the first stream
+// wave stamps events 20 + 2 ph (its first tile of phase ph computed) and 21 + 2 ph (its last)
 __device__ __forceinline__ void stamp(const Args& a, int l, int e) {
   if (DECODE_TRACE && (threadIdx.x & 63) == 0)
     a.trace[((int64_t)l * kEv + e) * a.ncu + blockIdx.x] = wall_clock64();
@@ -405,28 +409,29 @@ __device__ __forceinline__ float h2f_hi(uint32_t w) {
   return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
 }
 
-// one attention unit on the IO wave (its K / V rows already in LDS when `prefetched`)
+// one attention unit on the IO wave (its K / V rows already in LDS when `prefetched`); GRP query
+// heads per KV head at compile time, so every loop below is branch-free and its LDS reads are
+// issued in batches (a runtime head count left each read waiting for the previous one)
+template <int GRP>
 __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u, bool prefetched) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const CLayer& ly = layer_at(a, l);
-  const int S = a.S, C = a.C, grp = a.grp;
+  const int S = a.S, C = a.C;
   const int g = u / S, ch = u - g * S;
   const int L = a.L0 + 1;
   const int t0 = ch * C;
   const int n = min(C, L - t0);
   if (!prefetched) prefetch_kv(a, sm, ly, g, ch);
-  // q heads g*grp.., the new k / v row of head g (the q/k/v phase's output, other CUs' stores)
+  // q heads g*GRP.., the new k / v row of head g (the q/k/v phase's output, other CUs' stores):
+  // every word issued at once (one round trip), then RoPE
   const int64_t p = min(max(a.pos[0], (int64_t)0), a.cache_rows - 1);
   const float* cr = a.cosc + p * kD;
   const float* sr = a.sinc + p * kD;
-  const float c0 = (float)(_Float16)cr[lane], c1 = (float)(_Float16)cr[lane + 64];
-  const float s0 = (float)(_Float16)sr[lane], s1 = (float)(_Float16)sr[lane + 64];
-  // every q / k / v word of the unit issued at once (one round trip), then RoPE
-  uint32_t qw0[kMaxGrp], qw1[kMaxGrp];
+  uint32_t qw0[GRP], qw1[GRP];
 #pragma unroll
-  for (int h = 0; h < kMaxGrp; ++h) {
-    const _Float16* q = a.qkv + (int64_t)(g * grp + min(h, grp - 1)) * kD;
+  for (int h = 0; h < GRP; ++h) {
+    const _Float16* q = a.qkv + (int64_t)(g * GRP + h) * kD;
     qw0[h] = ld_sc1(q + (lane & ~1));
     qw1[h] = ld_sc1(q + 64 + (lane & ~1));
   }
@@ -434,15 +439,15 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
   const _Float16* vp = a.qkv + a.H + a.Hkv * kD + (int64_t)g * kD;
   const uint32_t k0w = ld_sc1(kp + (lane & ~1)), k1w = ld_sc1(kp + 64 + (lane & ~1));
   const uint32_t v0w = ld_sc1(vp + (lane & ~1)), v1w = ld_sc1(vp + 64 + (lane & ~1));
+  const float c0 = (float)(_Float16)cr[lane], c1 = (float)(_Float16)cr[lane + 64];
+  const float s0 = (float)(_Float16)sr[lane], s1 = (float)(_Float16)sr[lane + 64];
 #pragma unroll
-  for (int h = 0; h < kMaxGrp; ++h) {
-    if (h < grp) {
-      const float x0 = (lane & 1) ? h2f_hi(qw0[h]) : h2f_lo(qw0[h]);
-      const float x1 = (lane & 1) ? h2f_hi(qw1[h]) : h2f_lo(qw1[h]);
-      // rotate_half: out[d] = x[d] c[d] - x[d + 64] s[d]; out[d + 64] = x[d + 64] c[d + 64] + x[d] s[d + 64]
-      sm.qs[h][lane] = x0 * c0 + (-x1) * s0;
-      sm.qs[h][lane + 64] = x1 * c1 + x0 * s1;
-    }
+  for (int h = 0; h < GRP; ++h) {
+    const float x0 = (lane & 1) ? h2f_hi(qw0[h]) : h2f_lo(qw0[h]);
+    const float x1 = (lane & 1) ? h2f_hi(qw1[h]) : h2f_lo(qw1[h]);
+    // rotate_half: out[d] = x[d] c[d] - x[d + 64] s[d]; out[d + 64] = x[d + 64] c[d + 64] + x[d] s[d + 64]
+    sm.qs[h][lane] = x0 * c0 + (-x1) * s0;
+    sm.qs[h][lane + 64] = x1 * c1 + x0 * s1;
   }
   stamp(a, l, 14);
   const bool has_new = t0 + n == L;  // this chunk holds the new row L0
@@ -469,104 +474,119 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
   drain();
   if (has_new) {
     const int t = n - 1;
-    for (int kv = 0; kv < 2; ++kv) {
+    if (lane < 32) {
+      const int kv = lane >> 4, sg = lane & 15;
       const _Float16* src = kv ? sm.vnew : sm.knew;
-      if (lane < 16)
-        *reinterpret_cast<uint4*>(&sm.kvs[kv][kv_off(t, lane)]) =
-            *reinterpret_cast<const uint4*>(src + lane * 8);
+      *reinterpret_cast<uint4*>(&sm.kvs[kv][kv_off(t, sg)]) =
+          *reinterpret_cast<const uint4*>(src + sg * 8);
     }
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes visible to this wave's reads
   stamp(a, l, 15);
   // scores: lane = row t (and t + 64 for 128-row chunks); fp32 dot products over the 128 dims
-  float mloc[kMaxGrp];
+  float mloc[GRP];
 #pragma unroll
-  for (int h = 0; h < kMaxGrp; ++h) mloc[h] = -INFINITY;
+  for (int h = 0; h < GRP; ++h) mloc[h] = -INFINITY;
   for (int tb = 0; tb < C; tb += 64) {
     const int t = tb + lane;
-    float acc[kMaxGrp];
+    const int tr = min(t, n - 1);  // rows past the chunk read its last row, then are masked
+    float acc[GRP];
 #pragma unroll
-    for (int h = 0; h < kMaxGrp; ++h) acc[h] = 0.f;
-    if (t < n) {
-#pragma unroll 4
-      for (int seg = 0; seg < 16; ++seg) {
-        const h8 kk = *reinterpret_cast<const h8*>(&sm.kvs[0][kv_off(t, seg)]);
+    for (int h = 0; h < GRP; ++h) acc[h] = 0.f;
+    // 2 segments per step: a full unroll lets the scheduler hoist every q read (16 x GRP x 2
+    // float4) and spill
+#pragma unroll 2
+    for (int seg = 0; seg < 16; ++seg) {
+      const h8 kk = *reinterpret_cast<const h8*>(&sm.kvs[0][kv_off(tr, seg)]);
 #pragma unroll
-        for (int h = 0; h < kMaxGrp; ++h) {
-          if (h < grp) {
-            const float4 qa = *reinterpret_cast<const float4*>(&sm.qs[h][seg * 8]);
-            const float4 qb = *reinterpret_cast<const float4*>(&sm.qs[h][seg * 8 + 4]);
-            float s_ = acc[h];
-            s_ = fmaf(qa.x, (float)kk[0], s_);
-            s_ = fmaf(qa.y, (float)kk[1], s_);
-            s_ = fmaf(qa.z, (float)kk[2], s_);
-            s_ = fmaf(qa.w, (float)kk[3], s_);
-            s_ = fmaf(qb.x, (float)kk[4], s_);
-            s_ = fmaf(qb.y, (float)kk[5], s_);
-            s_ = fmaf(qb.z, (float)kk[6], s_);
-            s_ = fmaf(qb.w, (float)kk[7], s_);
-            acc[h] = s_;
-          }
-        }
+      for (int h = 0; h < GRP; ++h) {
+        const float4 qa = *reinterpret_cast<const float4*>(&sm.qs[h][seg * 8]);
+        const float4 qb = *reinterpret_cast<const float4*>(&sm.qs[h][seg * 8 + 4]);
+        float s_ = acc[h];
+        s_ = fmaf(qa.x, (float)kk[0], s_);
+        s_ = fmaf(qa.y, (float)kk[1], s_);
+        s_ = fmaf(qa.z, (float)kk[2], s_);
+        s_ = fmaf(qa.w, (float)kk[3], s_);
+        s_ = fmaf(qb.x, (float)kk[4], s_);
+        s_ = fmaf(qb.y, (float)kk[5], s_);
+        s_ = fmaf(qb.z, (float)kk[6], s_);
+        s_ = fmaf(qb.w, (float)kk[7], s_);
+        acc[h] = s_;
       }
     }
-    const float mk = (t < n && a.mask) ? (float)a.mask[t0 + t] : 0.f;
+    const float mk = a.mask ? (float)a.mask[t0 + tr] : 0.f;
 #pragma unroll
-    for (int h = 0; h < kMaxGrp; ++h) {
-      if (h < grp) {
-        float s_ = acc[h] / a.scale_div + mk;
-        s_ = (s_ != s_) ? s_ : fmaxf(s_, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
-        if (t >= n) s_ = -INFINITY;
-        sm.pb[h][t] = s_;
-        mloc[h] = fmaxf(mloc[h], s_);
-      }
+    for (int h = 0; h < GRP; ++h) {
+      float s_ = acc[h] / a.scale_div + mk;
+      s_ = (s_ != s_) ? s_ : fmaxf(s_, -3.402823466e38f);  // torch.max(w, finfo(fp32).min)
+      if (t >= n) s_ = -INFINITY;
+      sm.pb[h][t] = s_;
+      mloc[h] = fmaxf(mloc[h], s_);
     }
   }
   stamp(a, l, 16);
-  float m[kMaxGrp], lsum[kMaxGrp];
+  float m[GRP], lsum[GRP];
 #pragma unroll
-  for (int h = 0; h < kMaxGrp; ++h) {
-    m[h] = 0.f;
-    lsum[h] = 0.f;
-    if (h < grp) {
-      float v = mloc[h];
-      for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-      m[h] = v;
-      float s_ = 0.f;
-      for (int tb = 0; tb < C; tb += 64) {
-        const int t = tb + lane;
-        const float e = t < n ? expf(sm.pb[h][t] - v) : 0.f;
-        sm.pb[h][t] = e;
-        s_ += e;
-      }
-      for (int o = 32; o > 0; o >>= 1) s_ += __shfl_xor(s_, o);
-      lsum[h] = s_;
+  for (int h = 0; h < GRP; ++h) {
+    float v = mloc[h];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    m[h] = v;
+  }
+#pragma unroll
+  for (int h = 0; h < GRP; ++h) lsum[h] = 0.f;
+  for (int tb = 0; tb < C; tb += 64) {
+    const int t = tb + lane;
+#pragma unroll
+    for (int h = 0; h < GRP; ++h) {
+      const float e = t < n ? expf(sm.pb[h][t] - m[h]) : 0.f;  // rows past n: p = 0
+      sm.pb[h][t] = e;
+      lsum[h] += e;
     }
   }
+#pragma unroll
+  for (int h = 0; h < GRP; ++h) {
+    float v = lsum[h];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    lsum[h] = v;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
   stamp(a, l, 17);
-  // P V: lane owns dims 2 * lane, 2 * lane + 1 (segment lane / 4 of each row)
-  float o0[kMaxGrp], o1[kMaxGrp];
+  // P V: lane owns dims 2 * lane, 2 * lane + 1 (segment lane / 4 of each row), 8 rows per step
+  // (rows past n: p = 0 times the chunk's last row)
+  float o0[GRP], o1[GRP];
 #pragma unroll
-  for (int h = 0; h < kMaxGrp; ++h) o0[h] = o1[h] = 0.f;
-  for (int t = 0; t < n; ++t) {
-    const uint32_t vw = *reinterpret_cast<const uint32_t*>(
-        &sm.kvs[1][kv_off(t, lane >> 2) + 2 * (lane & 3)]);
-    const float v0 = h2f_lo(vw), v1 = h2f_hi(vw);
+  for (int h = 0; h < GRP; ++h) o0[h] = o1[h] = 0.f;
+  for (int tb = 0; tb < n; tb += 8) {
+    uint32_t vw[8];
 #pragma unroll
-    for (int h = 0; h < kMaxGrp; ++h) {
-      if (h < grp) {
-        const float pp = sm.pb[h][t];
+    for (int j = 0; j < 8; ++j)
+      vw[j] = *reinterpret_cast<const uint32_t*>(
+          &sm.kvs[1][kv_off(min(tb + j, n - 1), lane >> 2) + 2 * (lane & 3)]);
+    float4 pa[GRP], pq[GRP];
+#pragma unroll
+    for (int h = 0; h < GRP; ++h) {
+      pa[h] = *reinterpret_cast<const float4*>(&sm.pb[h][tb]);
+      pq[h] = *reinterpret_cast<const float4*>(&sm.pb[h][tb + 4]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v0 = h2f_lo(vw[j]), v1 = h2f_hi(vw[j]);
+#pragma unroll
+      for (int h = 0; h < GRP; ++h) {
+        const float4& pv = j < 4 ? pa[h] : pq[h];
+        const float pp = (j & 3) == 0 ? pv.x : (j & 3) == 1 ? pv.y : (j & 3) == 2 ? pv.z : pv.w;
         o0[h] = fmaf(pp, v0, o0[h]);
         o1[h] = fmaf(pp, v1, o1[h]);
       }
     }
   }
   stamp(a, l, 18);
-  const int64_t qh0 = (int64_t)g * grp;  // first query head of the group
+  const int64_t qh0 = (int64_t)g * GRP;  // first query head of the group
   if (S == 1) {
 #pragma unroll
-    for (int h = 0; h < kMaxGrp; ++h) {
-      if (h >= grp) break;
+    for (int h = 0; h < GRP; ++h) {
       const _Float16 r0 = (_Float16)(o0[h] / lsum[h]), r1 = (_Float16)(o1[h] / lsum[h]);
       st_sc1(a.abuf + (qh0 + h) * kD + 2 * lane,
              (uint32_t)__builtin_bit_cast(uint16_t, r0) |
@@ -577,16 +597,17 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
     return true;
   }
   // partials (sc1), count in; the last unit of the head merges
-  float* pp = a.part + ((int64_t)(g * S + ch) * grp) * (kD + 2);
+  float* pp = a.part + ((int64_t)(g * S + ch) * GRP) * (kD + 2);
 #pragma unroll
-  for (int h = 0; h < kMaxGrp; ++h) {
-    if (h >= grp) break;
+  for (int h = 0; h < GRP; ++h) {
     float* ph = pp + h * (kD + 2);
-    st_sc1(ph + 2 * lane, __builtin_bit_cast(uint32_t, o0[h]));
-    st_sc1(ph + 2 * lane + 1, __builtin_bit_cast(uint32_t, o1[h]));
+    const unsigned long long ov = (unsigned long long)__builtin_bit_cast(uint32_t, o0[h]) |
+                                  ((unsigned long long)__builtin_bit_cast(uint32_t, o1[h]) << 32);
+    __hip_atomic_store((gu64*)(ph + 2 * lane), ov, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lane == 0) {
-      st_sc1(ph + kD, __builtin_bit_cast(uint32_t, m[h]));
-      st_sc1(ph + kD + 1, __builtin_bit_cast(uint32_t, lsum[h]));
+      const unsigned long long mlv = (unsigned long long)__builtin_bit_cast(uint32_t, m[h]) |
+                                     ((unsigned long long)__builtin_bit_cast(uint32_t, lsum[h]) << 32);
+      __hip_atomic_store((gu64*)(ph + kD), mlv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   drain();
@@ -595,62 +616,61 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
   old = __builtin_amdgcn_readfirstlane(old);
   stamp(a, l, 19);
   if (old != S - 1) return true;
-  // merge (qlin_attn_decode's): weights w_s = exp(m_s - M), denominators sum_s w_s l_s.  The
-  // (m, l) of all S x grp partials arrive in one round of 8-B loads (lane j: partial j), the
-  // weights go through LDS (sm.pb), then the partial rows in rounds of <= 32 8-B loads per lane
-  const float* pg = a.part + (int64_t)g * S * grp * (kD + 2);
-  const int np = S * grp;  // partial j = s * grp + h (<= 512: S <= 64, grp <= 8)
-  float* pbf = &sm.pb[0][0];  // m (then the weight) of partial j at pbf[j], l at pbf[512 + j]
+  // merge (qlin_attn_decode's): weights w_j = exp(m_j - M_h), denominators sum_j w_j l_j over the
+  // S partials j = s * GRP + h of each head.  Lane j of a 64-partial round holds partial j's (m, l)
+  // (one round of 8-B loads; its head is lane % GRP), the head maxima / sums reduce over the lanes
+  // of one head (xor butterflies over strides >= GRP), the weights go to LDS, then the partial
+  // rows arrive in rounds of 32 8-B loads per lane
+  const float* pg = a.part + (int64_t)g * S * GRP * (kD + 2);
+  const int np = S * GRP;  // <= 512
+  float* pbf = &sm.pb[0][0];
+  float Ml = -INFINITY;
   for (int j0 = 0; j0 < np; j0 += 64) {
     const int j = min(j0 + lane, np - 1);
     const unsigned long long ml = ld_sc1_64(pg + (int64_t)j * (kD + 2) + kD);
-    if (j0 + lane < np) {
-      pbf[j0 + lane] = __builtin_bit_cast(float, (uint32_t)ml);
-      pbf[512 + j0 + lane] = __builtin_bit_cast(float, (uint32_t)(ml >> 32));
-    }
+    const float mj = j0 + lane < np ? __builtin_bit_cast(float, (uint32_t)ml) : -INFINITY;
+    pbf[j0 + lane] = mj;
+    pbf[512 + j0 + lane] = __builtin_bit_cast(float, (uint32_t)(ml >> 32));
+    Ml = fmaxf(Ml, mj);
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-  float den[kMaxGrp], acc0[kMaxGrp], acc1[kMaxGrp];
 #pragma unroll
-  for (int h = 0; h < kMaxGrp; ++h) {
-    den[h] = acc0[h] = acc1[h] = 0.f;
-    if (h < grp) {
-      float M = -INFINITY;
-      for (int s_ = 0; s_ < S; ++s_) M = fmaxf(M, pbf[s_ * grp + h]);
-      for (int s_ = 0; s_ < S; ++s_) {
-        const float w = expf(pbf[s_ * grp + h] - M);
-        den[h] += w * pbf[512 + s_ * grp + h];
-        pbf[s_ * grp + h] = w;
-      }
-    }
+  for (int o = 32; o >= GRP; o >>= 1) Ml = fmaxf(Ml, __shfl_xor(Ml, o));
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  float dl = 0.f;
+  for (int j0 = 0; j0 < np; j0 += 64) {
+    const float w = j0 + lane < np ? expf(pbf[j0 + lane] - Ml) : 0.f;
+    dl += w * (j0 + lane < np ? pbf[512 + j0 + lane] : 0.f);
+    pbf[j0 + lane] = w;
+  }
+#pragma unroll
+  for (int o = 32; o >= GRP; o >>= 1) dl += __shfl_xor(dl, o);
+  float den[GRP], acc0[GRP], acc1[GRP];
+#pragma unroll
+  for (int h = 0; h < GRP; ++h) {
+    den[h] = __shfl(dl, h);
+    acc0[h] = acc1[h] = 0.f;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
-  const int SR = 32 / grp;  // partial rows (s values) per round: <= 32 8-B loads per lane
+  constexpr int SR = 32 / GRP;  // partial rows (s values) per round: 32 8-B loads per lane
   for (int s0 = 0; s0 < S; s0 += SR) {
-    unsigned long long ov[32];
+    unsigned long long ov[SR][GRP];
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int s_ = min(s0 + k / grp, S - 1), h = k % grp;
-      ov[k] = ld_sc1_64(pg + ((int64_t)s_ * grp + h) * (kD + 2) + 2 * lane);
-    }
+    for (int k = 0; k < SR; ++k)
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int s_ = s0 + k / grp, h = k % grp;
-      if (s_ < S) {
+      for (int h = 0; h < GRP; ++h)
+        ov[k][h] = ld_sc1_64(pg + ((int64_t)min(s0 + k, S - 1) * GRP + h) * (kD + 2) + 2 * lane);
 #pragma unroll
-        for (int hh = 0; hh < kMaxGrp; ++hh) {
-          if (hh == h) {
-            const float w = pbf[s_ * grp + hh];
-            acc0[hh] = fmaf(w, __builtin_bit_cast(float, (uint32_t)ov[k]), acc0[hh]);
-            acc1[hh] = fmaf(w, __builtin_bit_cast(float, (uint32_t)(ov[k] >> 32)), acc1[hh]);
-          }
-        }
+    for (int k = 0; k < SR; ++k) {
+#pragma unroll
+      for (int h = 0; h < GRP; ++h) {
+        const float w = s0 + k < S ? pbf[(s0 + k) * GRP + h] : 0.f;
+        acc0[h] = fmaf(w, __builtin_bit_cast(float, (uint32_t)ov[k][h]), acc0[h]);
+        acc1[h] = fmaf(w, __builtin_bit_cast(float, (uint32_t)(ov[k][h] >> 32)), acc1[h]);
       }
     }
   }
 #pragma unroll
-  for (int h = 0; h < kMaxGrp; ++h) {
-    if (h >= grp) break;
+  for (int h = 0; h < GRP; ++h) {
     const _Float16 r0 = (_Float16)(acc0[h] / den[h]), r1 = (_Float16)(acc1[h] / den[h]);
     st_sc1(a.abuf + (qh0 + h) * kD + 2 * lane,
            (uint32_t)__builtin_bit_cast(uint16_t, r0) |
@@ -659,6 +679,15 @@ __device__ __forceinline__ bool attn_unit(const Args& a, Smem& sm, int l, int u,
   drain();
   if (lane == 0) add_agent(cnt_attn(a, l), 1);
   return true;
+}
+
+__device__ __forceinline__ bool attn_unit_g(const Args& a, Smem& sm, int l, int u, bool pre) {
+  switch (a.grp) {
+    case 1: return attn_unit<1>(a, sm, l, u, pre);
+    case 2: return attn_unit<2>(a, sm, l, u, pre);
+    case 4: return attn_unit<4>(a, sm, l, u, pre);
+    default: return attn_unit<8>(a, sm, l, u, pre);
+  }
 }
 
 __device__ __forceinline__ void io_wave(const Args& a, Smem& sm) {
@@ -690,7 +719,7 @@ __device__ __forceinline__ void io_wave(const Args& a, Smem& sm) {
       stamp(a, l, 3);
       for (int u = u0; u < U; ++u) {
         if (unit_cu(u, U, a.ncu) != c) continue;
-        if (!attn_unit(a, sm, l, u, u == u0)) return;
+        if (!attn_unit_g(a, sm, l, u, u == u0)) return;
       }
       stamp(a, l, 4);
     }
@@ -726,13 +755,6 @@ __device__ __forceinline__ void io_wave(const Args& a, Smem& sm) {
 // ---------------------------------------------------------------------------------------------
 // a wave's position in its tile sequence: layer, phase, flat index t of the CU's phase tiles
 // (row-major over its rows), end of the wave's run in this phase
-struct Cur {
-  int l, ph, t, tend, T, i, kt, Kt, Gs;
-  const gu32* qw;  // this run's phase matrix (uniform)
-  const gu32* sz;
-  bool done;       // load cursor past the wave's last tile: it repeats that tile
-};
-
 __device__ __forceinline__ void run_of(const Args& a, int ph, int wave, int& t, int& tend, int& T) {
   const int n = rows_of(a.R[ph], blockIdx.x, a.ncu);
   T = n * a.Kt[ph];
@@ -740,37 +762,79 @@ __device__ __forceinline__ void run_of(const Args& a, int ph, int wave, int& t, 
   tend = (int)(((int64_t)(wave + 1) * T) / kStream);
 }
 
-// the next non-empty run after (c.l, c.ph), or c.l == nl at the end; the run's operands come from
-// the layer table through the constant address space (scalar loads: no vmcnt wait in the stream)
-__device__ __forceinline__ void next_run(const Args& a, Cur& c, int wave) {
+// the next non-empty run after (l, ph) of this wave; false at the end of the launch
+__device__ __forceinline__ bool next_run(const Args& a, int wave, int& l, int& ph, int& t,
+                                         int& tend, int& T) {
   for (;;) {
-    if (++c.ph == kPhases) {
-      c.ph = 0;
-      if (++c.l == a.nl) return;
+    if (++ph == kPhases) {
+      ph = 0;
+      if (++l == a.nl) return false;
     }
-    run_of(a, c.ph, wave, c.t, c.tend, c.T);
-    if (c.t < c.tend) break;
+    run_of(a, ph, wave, t, tend, T);
+    if (t < tend) return true;
   }
-  c.Kt = a.Kt[c.ph];
-  c.Gs = a.Gs[c.ph];
-  c.i = c.t / c.Kt;
-  c.kt = c.t - c.i * c.Kt;
-  const CLayer& ly = layer_at(a, c.l);
-  c.qw = (const gu32*)ly.qw[c.ph];
-  c.sz = (const gu32*)ly.sz[c.ph];
 }
 
-// advance one tile; true when the tile just passed ended an item (a row or the run).  Past the
-// wave's last tile the load cursor stays on its last row (done), so every slot is loaded
-// unconditionally
-__device__ __forceinline__ bool advance(const Args& a, Cur& c, int wave) {
-  if (c.done) {
-    // keep loading valid tiles of the last row, each at a new address: a load the compiler can
-    // prove equal to the previous one is replaced by a copy of its result (a vmcnt(0) wait)
+// load cursor: the tile whose lane pieces the next load() fetches.  Per tile only kt and, at a
+// row end, two row pointers move; a run's operands come from the layer table through the
+// constant address space (scalar loads: no vmcnt wait in the stream).  Past the wave's last tile
+// (done) it cycles through that row's tiles: valid addresses that differ from load to load (a load
+// the compiler can prove equal to the previous one becomes a copy of its result: a vmcnt(0) wait)
+struct LoadCur {
+  int l, ph, t, tend, T, kt, Kt, left;
+  int64_t rstep_qw, rstep_sz;  // words between the CU's consecutive rows of this phase
+  const gu32* row_qw;          // tile 0 of the current row (uniform; + lane * BITS at the load)
+  const gu32* row_sz;          // (scale, zero) words of the current row (uniform; + n_in)
+  bool done;
+};
+
+template <int BITS>
+__device__ __forceinline__ void enter_run(const Args& a, LoadCur& c) {
+  c.Kt = a.Kt[c.ph];
+  const int Gs = a.Gs[c.ph];
+  const int i = c.t / c.Kt;
+  c.kt = c.t - i * c.Kt;
+  const int64_t r = blockIdx.x + (int64_t)i * a.ncu;
+  const CLayer& ly = layer_at(a, c.l);
+  c.row_qw = (const gu32*)ly.qw[c.ph] + r * c.Kt * (64 * BITS);
+  c.row_sz = (const gu32*)ly.sz[c.ph] + r * Gs * kTileN;
+  c.rstep_qw = (int64_t)a.ncu * c.Kt * (64 * BITS);
+  c.rstep_sz = (int64_t)a.ncu * Gs * kTileN;
+}
+
+template <int BITS>
+__device__ __forceinline__ void advance_load(const Args& a, LoadCur& c, int wave) {
+  if (c.done || --c.left == 0) {
+    c.done = true;
     c.kt = c.kt + 1 == c.Kt ? 0 : c.kt + 1;
-    return false;
+    return;
   }
-  const Cur prev = c;
+  ++c.t;
+  if (++c.kt == c.Kt) {
+    c.kt = 0;
+    c.row_qw += c.rstep_qw;
+    c.row_sz += c.rstep_sz;
+  }
+  if (c.t == c.tend) {
+    next_run(a, wave, c.l, c.ph, c.t, c.tend, c.T);  // left > 0: a run follows
+    enter_run<BITS>(a, c);
+  }
+}
+
+// compute cursor: the tile the next compute() multiplies, and where its item (a row's share of
+// this wave) ends
+struct CompCur {
+  int l, ph, t, tend, T, kt, Kt, i;
+};
+
+__device__ __forceinline__ void enter_run(const Args& a, CompCur& c) {
+  c.Kt = a.Kt[c.ph];
+  c.i = c.t / c.Kt;
+  c.kt = c.t - c.i * c.Kt;
+}
+
+// one tile on; true when the tile just passed ended an item (its row, or the wave's run)
+__device__ __forceinline__ bool advance_comp(const Args& a, CompCur& c, int wave) {
   ++c.t;
   bool end = false;
   if (++c.kt == c.Kt) {
@@ -779,12 +843,8 @@ __device__ __forceinline__ bool advance(const Args& a, Cur& c, int wave) {
     end = true;
   }
   if (c.t == c.tend) {
-    next_run(a, c, wave);
     end = true;
-    if (c.l == a.nl) {
-      c = prev;
-      c.done = true;
-    }
+    if (next_run(a, wave, c.l, c.ph, c.t, c.tend, c.T)) enter_run(a, c);
   }
   return end;
 }
@@ -829,24 +889,30 @@ __device__ __forceinline__ void stream_wave(const Args& a, Smem& sm, int wave) {
   total *= a.nl;
   if (total == 0) return;
 
-  Cur lc;
+  LoadCur lc;
   lc.l = 0;
   lc.ph = -1;
   lc.done = false;
-  next_run(a, lc, wave);  // total > 0: a run exists
-  Cur cc = lc;
+  lc.left = total;
+  next_run(a, wave, lc.l, lc.ph, lc.t, lc.tend, lc.T);  // total > 0: a run exists
+  enter_run<BITS>(a, lc);
+  CompCur cc;
+  cc.l = lc.l;
+  cc.ph = lc.ph;
+  cc.t = lc.t;
+  cc.tend = lc.tend;
+  cc.T = lc.T;
+  enter_run(a, cc);
   auto group_of_tile = [&](int kt) {
     return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
   };
   WTile<BITS, GPT> wt[PF];
   auto load = [&](int u) {
-    const int64_t r = cu + lc.i * a.ncu;  // global tile row
-    wt[u].pc = load_piece_g<BITS>(lc.qw + (r * lc.Kt + lc.kt) * (64 * BITS) + lane * BITS);
-    const gu32* sz = lc.sz + r * lc.Gs * kTileN + n_in;
-    const int g0 = group_of_tile(lc.kt);
+    wt[u].pc = load_piece_g<BITS>(lc.row_qw + lc.kt * (64 * BITS) + lane * BITS);
+    const gu32* sz = lc.row_sz + group_of_tile(lc.kt) * kTileN + n_in;
 #pragma unroll
-    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = sz[(g0 + s) * kTileN];
-    advance(a, lc, wave);
+    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = sz[s * kTileN];
+    advance_load<BITS>(a, lc, wave);
   };
 
   const Magics mg = make_magics<BITS>();
@@ -858,6 +924,7 @@ __device__ __forceinline__ void stream_wave(const Args& a, Smem& sm, int wave) {
   auto flush = [&](int ph, int i, int T, int Kt) {
     const int lo = i * Kt, hi = lo + Kt;
     int nsplit = 0, j = 0;
+#pragma unroll
     for (int w = 0; w < kStream; ++w) {
       const int b0 = (int)(((int64_t)w * T) / kStream), b1 = (int)(((int64_t)(w + 1) * T) / kStream);
       if (max(b0, lo) < min(b1, hi)) {
@@ -922,14 +989,19 @@ __device__ __forceinline__ void stream_wave(const Args& a, Smem& sm, int wave) {
     step(std::integral_constant<int, 2>{});
     step(std::integral_constant<int, 3>{});
     const int ph = cc.ph, i = cc.i, T = cc.T, Kt = cc.Kt;
-    if (__builtin_expect(advance(a, cc, wave), 0)) {
+    if (DECODE_TRACE && wave == 0) {
+      if (cc.t == (int)(((int64_t)wave * T) / kStream)) stamp(a, cc.l, 20 + 2 * ph);
+      if (cc.t + 1 == cc.tend) stamp(a, cc.l, 21 + 2 * ph);
+    }
+    if (__builtin_expect(advance_comp(a, cc, wave), 0)) {
       flush(ph, i, T, Kt);
       acc = f4{0.f, 0.f, 0.f, 0.f};
     }
   };
 
-  // every slot is loaded unconditionally (the load cursor repeats the wave's last tile once it is
-  // past it), so hipcc counts the loads with vmcnt(N) instead of draining at each branch
+  // every slot is loaded unconditionally (the load cursor cycles through the wave's last row once
+  // it is past its last tile), so hipcc counts the loads with vmcnt(N) instead of draining at
+  // each branch
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u);
   for (int base = 0; base < total; base += PF) {
@@ -952,6 +1024,10 @@ __global__ __launch_bounds__(64 * kWaves) void decode_kernel(const Args a) {
   }
   if (threadIdx.x < kMaxRows) sm.rowcnt[threadIdx.x] = 0;
   __syncthreads();
+  if (DECODE_STREAM_ONLY && wave == 0) {
+    __hip_atomic_store(&sm.xready, 1 << 30, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
   if (wave == 0) {
     // the IO wave's serial work (staging, norms, attention, publishing) is every CU's critical
     // path; the stream wave sharing its SIMD yields issue slots to it

@@ -140,6 +140,20 @@ class DecodeEngine:
                                    dtype=torch.uint8, device=device)
         return self._ws
 
+    def _rope(self, hidden_states, L):
+        """The fp32 cos / sin cache the kernel reads (one for all layers: checked equal once per
+        cache version, never per step — a device comparison per step would sync the host)."""
+        caches = [layer.self_attn._rope_cache(hidden_states, L) for layer in self.layers]
+        key = tuple((c.data_ptr(), c._version, s_.data_ptr(), s_._version) for c, s_ in caches)
+        if key != getattr(self, "_rope_key", None):
+            c0, s0 = caches[0]
+            for c, s_ in caches[1:]:
+                if (c.data_ptr() != c0.data_ptr() and not torch.equal(c, c0)) or \
+                        (s_.data_ptr() != s0.data_ptr() and not torch.equal(s_, s0)):
+                    raise ValueError("DecodeEngine: layers with different rotary caches")
+            self._rope_key = key
+        return caches[0]
+
     @torch.no_grad()
     def step(self, hidden_states, position_ids, past_key_values=None, attention_mask=None):
         """hidden_states fp16 [1, 1, H]; position_ids int64 (one position); past_key_values: one
@@ -150,12 +164,7 @@ class DecodeEngine:
         dev = hidden_states.device
         bufs, L0 = self._caches(past_key_values, dev)
         L = L0 + 1
-        at0 = self.layers[0].self_attn
-        cos_c, sin_c = at0._rope_cache(hidden_states, L)
-        for layer in self.layers[1:]:
-            c2, s2 = layer.self_attn._rope_cache(hidden_states, L)
-            if c2.data_ptr() != cos_c.data_ptr() and not torch.equal(c2, cos_c):
-                raise ValueError("DecodeEngine: layers with different rotary caches")
+        cos_c, sin_c = self._rope(hidden_states, L)
         table = self._pointer_table(bufs, dev)
         ws = self._workspace(dev, L)
         x = hidden_states.reshape(-1).contiguous()
