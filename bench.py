@@ -245,7 +245,7 @@ def main():
                         y.data_ptr(), M, N, K, bits, group, st)
             else:
                 rc = fn(qw.data_ptr(), qsz.data_ptr(), fl_, x.data_ptr(), None, y.data_ptr(),
-                        M, N, K, bits, group, None, st)
+                        M, N, K, bits, group, None, 0, st)
             if rc != 0:
                 raise RuntimeError(f"kernel failed: {rc}")
 

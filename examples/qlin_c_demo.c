@@ -61,7 +61,7 @@ static int abi_only(void) {
   /* every entry point validates its arguments before touching a device */
   int bad = 0;
   bad |= qlin_gemv_f16(NULL, NULL, 0, NULL, NULL, NULL, 1, 16, 64, 4, 64, NULL) != 1;
-  bad |= qlin_gemm_f16(NULL, NULL, 0, NULL, NULL, NULL, 8, 16, 64, 4, 64, NULL, NULL) != 1;
+  bad |= qlin_gemm_f16(NULL, NULL, 0, NULL, NULL, NULL, 8, 16, 64, 4, 64, NULL, 0, NULL) != 1;
   bad |= qlin_dequant_f16(NULL, NULL, 0, 16, 64, 4, 64, NULL, NULL) != 1;
   bad |= qlin_pack_codes(NULL, 16, 64, 4, NULL, NULL) != 1;
   printf("abi %d, argument validation %s\n", qlin_abi_version(), bad ? "FAILED" : "ok");

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 6
+#define QLIN_ABI_VERSION 7
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -135,18 +135,19 @@ int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, in
  *   qlin_gemv_f16: matrix-core GEMV, 1 <= M <= 16 (decode / small batches).
  *   qlin_gemm_f16: MFMA (v_mfma_f32_*_f16) tiles, any M >= 1 (prefill / PPL windows).
  *   qlin_linear_f16: picks from M: GEMV for M <= 64 (16-row chunks), MFMA GEMM above.
- *   workspace (qlin_gemm_f16): NULL, or at least qlin_linear_workspace_bytes(M, N, K, bits, group,
- *     0) bytes of device memory (no alignment beyond 256 B, contents need not be initialised):
- *     with it, launches whose grid of 64 x 128 blocks leaves most CUs idle split K over up to 8
- *     block groups and reduce the fp32 partials in a second pass (fixed order: deterministic,
- *     within fp32 rounding of the unsplit launch); without it they run unsplit.
+ *   workspace / workspace_bytes (qlin_gemm_f16): NULL / 0, or a device buffer (256-B aligned,
+ *     contents need not be initialised) of workspace_bytes bytes: when that is at least
+ *     qlin_linear_workspace_bytes(M, N, K, bits, group, 0), launches whose grid of 64 x 128 blocks
+ *     leaves most CUs idle split K over up to 8 block groups and reduce the fp32 partials in a
+ *     second pass (fixed order: deterministic, within fp32 rounding of the unsplit launch); with
+ *     a smaller (or no) buffer they run unsplit — the call never writes past workspace_bytes.
  */
 int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                   const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
                   int group, void* stream);
 int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                   const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
-                  int group, void* workspace, void* stream);
+                  int group, void* workspace, int64_t workspace_bytes, void* stream);
 /*
  * Strided batch of independent decode products in one launch:
  *   y[b] = x[b] @ W_dq[b]^T (+ bias[b]),  b < batch (<= 65535), 1 <= M <= 16,
@@ -157,8 +158,10 @@ int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const
  * several independent QuantLinear modules of one shape at once (e.g. one decode step over the
  * modules of a ring of layers' weights); one kernel boundary per batch instead of per matrix.
  * x_stride / bias_stride may be 0 (one activation / bias shared by every problem); other strides
- * smaller than one problem's extent return QLIN_EINVAL.  M <= 4 with K % 512 == 0 and group a
- * multiple of 128 (or 32 / 64) runs the streaming kernel: each output is one MFMA chain in k
+ * smaller than one problem's extent return QLIN_EINVAL.  M <= 4 with K % 512 == 0, group a
+ * multiple of 128 (or 32 / 64) and 16-B aligned operands (qweight / qsz / x bases 16-B aligned,
+ * qweight_stride and qsz_stride multiples of 4 words, x_stride a multiple of 8) runs the streaming
+ * kernel: each output is one MFMA chain in k
  * order, bit-identical to qlin_gemm_f16 without workspace; other shapes run one qlin_gemv_f16
  * launch per problem.
  */
@@ -201,9 +204,11 @@ int qlin_gemm_block_cols(int64_t M, int64_t N, int bits);
  * block recomputes the token's min / max; x 16-byte aligned, K % 8 == 0); otherwise the quantizer
  * kernel writes x_dq to `workspace` (fp16 [M, K], required then) before the GEMV / GEMM.
  * Same kernels and dispatch as qlin_linear_f16 (GEMV for M <= 64, MFMA GEMM above).
- * workspace: NULL (only without the act quantizer kernel) or at least
- * qlin_linear_workspace_bytes(M, N, K, bits, group, act_bits) bytes: the x_dq region, then the
- * split-K partials of qlin_gemm_f16 (with too little the call writes past the buffer).
+ * workspace / workspace_bytes: NULL / 0 (only without the act quantizer kernel), or a buffer of
+ * workspace_bytes bytes laid out as the x_dq region (when the quantizer kernel runs; a buffer
+ * smaller than that region returns QLIN_EINVAL), then the split-K partials of qlin_gemm_f16 (run
+ * unsplit when the rest is smaller than they need).  qlin_linear_workspace_bytes(M, N, K, bits,
+ * group, act_bits) is the full size; the call never writes past workspace_bytes.
  */
 #define QLIN_EP_NONE     0
 #define QLIN_EP_RESIDUAL 1
@@ -211,7 +216,8 @@ int qlin_gemm_block_cols(int64_t M, int64_t N, int bits);
 int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                        const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M,
                        int64_t N, int64_t K, int bits, int group, int epilogue, int act_bits,
-                       int act_flags, uint16_t* workspace, void* stream);
+                       int act_flags, uint16_t* workspace, int64_t workspace_bytes,
+                       void* stream);
 
 /*
  * RMSNorm + packed linear for ONE token row in one launch (the decoder layer's

@@ -607,12 +607,21 @@ extern "C" int64_t qlin_linear_workspace_bytes(int64_t M, int64_t N, int64_t K, 
   return act_ws_bytes(M, N, K, act_bits) + splitk_bytes(M, N, splitk_parts(M, N, K, bits));
 }
 
+// the split-K workspace when the caller's buffer holds this launch's partials, else nullptr
+// (the launch then runs unsplit: a short buffer is never written past its end)
+void* splitk_ws_of(void* ws, int64_t ws_bytes, int64_t M, int64_t N, int64_t K, int bits) {
+  if (!ws || ws_bytes <= 0 || M < 1 || N < 1 || N > (1 << 30) || K < 1) return nullptr;
+  const int S = splitk_parts(M, N, K, bits);
+  return S > 1 && ws_bytes >= splitk_bytes(M, N, S) ? ws : nullptr;
+}
+
 extern "C" int qlin_gemm_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                              const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
                              int64_t N, int64_t K, int bits, int group, void* workspace,
-                             void* stream) {
+                             int64_t workspace_bytes, void* stream) {
+  if (workspace_bytes < 0) return QLIN_EINVAL;
   return gemm_ep(qweight, qsz, flags, x, bias, nullptr, y, M, N, K, bits, group, kEpNone, stream,
-                 workspace);
+                 splitk_ws_of(workspace, workspace_bytes, M, N, K, bits));
 }
 
 extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
@@ -630,14 +639,16 @@ extern "C" int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int
     }
     return QLIN_OK;
   }
-  return qlin_gemm_f16(qweight, qsz, flags, x, bias, y, M, N, K, bits, group, nullptr, stream);
+  return qlin_gemm_f16(qweight, qsz, flags, x, bias, y, M, N, K, bits, group, nullptr, 0, stream);
 }
 
 extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                                   const uint16_t* x, const uint16_t* bias,
                                   const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
                                   int64_t K, int bits, int group, int epilogue, int act_bits,
-                                  int act_flags, uint16_t* workspace, void* stream) {
+                                  int act_flags, uint16_t* workspace, int64_t workspace_bytes,
+                                  void* stream) {
+  if (workspace_bytes < 0 || (workspace_bytes > 0 && !workspace)) return QLIN_EINVAL;
   if (epilogue < kEpNone || epilogue > kEpSiluMul) return QLIN_EINVAL;
   if (epilogue == kEpResidual && !residual) return QLIN_EINVAL;
   if (epilogue == kEpSiluMul && N % kTileN) return QLIN_EINVAL;
@@ -651,7 +662,7 @@ extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, 
   const bool fuse_act = act_bits && M <= kSkinnyMaxM && N <= kActFuseMaxN;
   const int64_t act_bytes = act_ws_bytes(M, N, K, act_bits);
   if (act_bits && !fuse_act) {
-    if (!workspace) return QLIN_EINVAL;
+    if (!workspace || workspace_bytes < act_bytes) return QLIN_EINVAL;
     const int rc = qlin_quantize(x, QLIN_F16, M, K, act_bits, (int)K,
                                  act_flags & (QLIN_SYMMETRIC | QLIN_DISABLE_ZERO_POINT), nullptr,
                                  nullptr, workspace, nullptr, nullptr, nullptr, nullptr, stream);
@@ -670,7 +681,10 @@ extern "C" int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, 
     return QLIN_OK;
   }
   return gemm_ep(qweight, qsz, flags, x, bias, residual, y, M, N, K, bits, group, epilogue,
-                 stream, workspace ? (void*)((char*)workspace + act_bytes) : nullptr);
+                 stream,
+                 workspace ? splitk_ws_of((char*)workspace + act_bytes, workspace_bytes - act_bytes,
+                                          M, N, K, bits)
+                           : nullptr);
 }
 
 // CUs of the current device, cached per device id (the first call per device queries it; racing

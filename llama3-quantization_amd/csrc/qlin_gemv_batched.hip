@@ -310,9 +310,14 @@ extern "C" int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_st
   if (batch == 0 || N == 0) return QLIN_OK;
   hipStream_t st = (hipStream_t)stream;
   // the streaming kernel: M <= 4, whole tiles (a multiple of 4 per row), group a multiple of 128
-  // or 32 / 64
-  if (M <= 4 && K % kTileK == 0 && (group % kTileK == 0 || group == 32 || group == 64) &&
-      Kt % 4 == 0) {
+  // or 32 / 64, and every problem's operands 16-B aligned (it issues 16-B loads of the codes, of a
+  // round's (scale, zero) words and of x rows): qweight / qsz / x bases 16-B aligned, strides whole
+  // 16-B units (qweight / qsz words % 4, x halfs % 8); anything else takes the per-problem path
+  const bool aligned = ((uintptr_t)qweight & 15) == 0 && ((uintptr_t)qsz & 15) == 0 &&
+                       ((uintptr_t)x & 15) == 0 && qweight_stride % 4 == 0 &&
+                       qsz_stride % 4 == 0 && x_stride % 8 == 0 && (M == 1 || K % 8 == 0);
+  if (aligned && M <= 4 && K % kTileK == 0 &&
+      (group % kTileK == 0 || group == 32 || group == 64) && Kt % 4 == 0) {
     StreamArgs a;
     a.qw = qweight; a.qsz = qsz; a.x = (const _Float16*)x; a.bias = (const _Float16*)bias;
     a.y = (_Float16*)y;

@@ -16,7 +16,7 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -44,13 +44,13 @@ SIGNATURES = {
     "qlin_pack_codes": ([_p, _l, _l, _i, _p, _p], _i),
     "qlin_dequant_f16": ([_p, _p, _i, _l, _l, _i, _i, _p, _p], _i),
     "qlin_gemv_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
-    "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _p], _i),
+    "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _l, _p], _i),
     "qlin_gemv_batched_f16": ([_p, _l, _p, _l, _i, _p, _l, _p, _l, _p, _l, _l, _l, _l, _l, _i, _i,
                                _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_block_cols": ([_l, _l, _i], _i),
     "qlin_linear_workspace_bytes": ([_l, _l, _l, _i, _i, _i], _l),
-    "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _i, _i, _p, _p],
+    "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _i, _i, _p, _l, _p],
                            _i),
     "qlin_rmsnorm_f16": ([_p, _p, _p, _l, _l, ctypes.c_float, _p], _i),
     "qlin_rope_f16": ([_p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _l, _i, _i, _i, _p], _i),
@@ -359,7 +359,7 @@ def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0, split=True):
     M = x.numel() // K if K else 0
     ws = _workspace(x.device, M, N, K, bits, group) if (split and M) else None
     return _linear_call("qlin_gemm_f16", x, qweight, qsz, bias, N, K, bits, group, flags,
-                        extra=(_ptr(ws),))
+                        extra=(_ptr(ws), 0 if ws is None else ws.numel()))
 
 
 SKINNY_MAX_M = 64  # qlin_linear_*: M <= this runs the GEMV kernel
@@ -405,7 +405,8 @@ def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NON
     ws = _workspace(x.device, M, N, K, bits, group, act_bits)
     rc = load_library().qlin_linear_ep_f16(_ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(bias),
                                            _ptr(residual), _ptr(y), M, N, K, bits, group,
-                                           epilogue, act_bits, act_flags, _ptr(ws), _stream(x))
+                                           epilogue, act_bits, act_flags, _ptr(ws),
+                                           0 if ws is None else ws.numel(), _stream(x))
     _check(rc, "qlin_linear_ep_f16")
     return y
 

@@ -62,11 +62,11 @@ def test_epilogue_argument_checks():
     P = lambda a: a.data_ptr()
     ep = lib.qlin_linear_ep_f16
     assert ep(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 32, 128, 4, 128, qlin.EP_RESIDUAL,
-              0, 0, None, None) == 1  # residual missing
+              0, 0, None, 0, None) == 1  # residual missing
     assert ep(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 24, 128, 4, 128, qlin.EP_SILU_MUL,
-              0, 0, None, None) == 1  # N % 16
+              0, 0, None, 0, None) == 1  # N % 16
     assert ep(P(qw), P(qsz), fl, P(x), None, None, P(y), 1, 32, 128, 4, 128, 7,
-              0, 0, None, None) == 1  # unknown epilogue
+              0, 0, None, 0, None) == 1  # unknown epilogue
 
 
 @pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (3, 768), (5, 14336), (64, 4096)])

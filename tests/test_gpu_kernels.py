@@ -195,7 +195,7 @@ def test_invalid_arguments_raise():
     assert lib.qlin_gemv_f16(qw.data_ptr(), qsz.data_ptr(), 0, x.data_ptr(), None, y.data_ptr(),
                              17, N, K, 4, group, None) == 1
     assert lib.qlin_gemm_f16(None, qsz.data_ptr(), 0, x.data_ptr(), None, y.data_ptr(),
-                             1, N, K, 4, group, None, None) == 1
+                             1, N, K, 4, group, None, 0, None) == 1
 
 
 @pytest.mark.parametrize("bits,group", [(4, 128), (3, 64), (2, 64), (8, 128)])

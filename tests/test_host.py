@@ -41,7 +41,7 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     # every entry point validates before touching the device
     assert lib.qlin_dequant_f16(None, None, 0, 16, 64, 4, 64, None, None) == 1
     assert lib.qlin_gemv_f16(None, None, 0, None, None, None, 1, 16, 64, 4, 64, None) == 1
-    assert lib.qlin_gemm_f16(None, None, 0, None, None, None, 8, 16, 64, 4, 64, None, None) == 1
+    assert lib.qlin_gemm_f16(None, None, 0, None, None, None, 8, 16, 64, 4, 64, None, 0, None) == 1
     assert lib.qlin_quantize(None, 0, 4, 64, 4, 64, 0, None, None, None, None, None, None, None,
                              None) == 1
     assert lib.qlin_fake_quant(None, 0, None, None, 4, 64, 4, 64, 0, None, None, None, None) == 1
@@ -51,14 +51,16 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 17, 16, 64, 4, 64, None) == 1  # M > 16
     assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 1, 16, 64, 5, 64, None) == 1   # bits
     assert lib.qlin_gemv_f16(p, p, 0, p, None, p, 1, 16, 128, 4, 96, None) == 1  # group | K
-    assert lib.qlin_gemm_f16(p, p, 0, p, None, p, 8, 16, 64, 4, 48, None, None) == 1  # group % 32
+    assert lib.qlin_gemm_f16(p, p, 0, p, None, p, 8, 16, 64, 4, 48, None, 0, None) == 1  # group % 32
+    assert lib.qlin_gemm_f16(p, p, 0, p, None, p, 8, 16, 64, 4, 64, None, -1, None) == 1  # ws bytes
     assert lib.qlin_linear_f16(p, p, 0, p, None, p, 8, -1, 64, 4, 64, None) == 1  # N < 0
     assert lib.qlin_dequant_f16(p, p, 0, 16, 64, 3, 128, p, None) == 1  # group > K
     ep = lib.qlin_linear_ep_f16
-    assert ep(p, p, 0, p, None, None, p, 1, 16, 64, 4, 64, 1, 0, 0, None, None) == 1  # residual
-    assert ep(p, p, 0, p, None, None, p, 1, 24, 64, 4, 64, 2, 0, 0, None, None) == 1  # N % 16
-    assert ep(p, p, 0, p, None, None, p, 1, 16, 64, 4, 64, 0, 9, 0, None, None) == 1  # act bits
-    assert ep(p, p, 0, p, None, None, p, 100, 16, 64, 4, 64, 0, 8, 0, None, None) == 1  # no ws
+    assert ep(p, p, 0, p, None, None, p, 1, 16, 64, 4, 64, 1, 0, 0, None, 0, None) == 1  # residual
+    assert ep(p, p, 0, p, None, None, p, 1, 24, 64, 4, 64, 2, 0, 0, None, 0, None) == 1  # N % 16
+    assert ep(p, p, 0, p, None, None, p, 1, 16, 64, 4, 64, 0, 9, 0, None, 0, None) == 1  # act bits
+    assert ep(p, p, 0, p, None, None, p, 100, 16, 64, 4, 64, 0, 8, 0, None, 0, None) == 1  # no ws
+    assert ep(p, p, 0, p, None, None, p, 100, 16, 64, 4, 64, 0, 8, 0, p, 64, None) == 1  # short ws
     assert lib.qlin_pack_codes(None, 16, 64, 4, None, None) == 1
     assert lib.qlin_pack_codes(p, 16, 48, 4, p, None) == 1  # K % 32
     assert lib.qlin_pack_codes(p, 16, 64, 5, p, None) == 1  # bits
