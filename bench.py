@@ -101,6 +101,12 @@ def parse():
     ap.add_argument("--no-other-mode", action="store_true",
                     help="skip timing the other GEMV mode (batched / launches)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-decode-layer", action="store_true",
+                    help="skip the decode-layer line (configs[1] inside the model, DESIGN.md §5)")
+    ap.add_argument("--decode-layers", type=int, default=8)
+    ap.add_argument("--decode-kv", type=int, default=512)
+    ap.add_argument("--decode-engine", action="store_true",
+                    help="also time the persistent one-launch decode engine")
     return ap.parse_args()
 
 
@@ -169,6 +175,112 @@ def cpu_baseline(M, N, K, bits, group, seconds):
                        f"torch.set_num_threads({threads}) = the CPUs this process may use"),
             "quantize_every_call_ms": round(statistics.median(calls) * 1e3, 2),
             "quantize_every_call_calls": len(calls)}
+
+
+def decode_layer_bytes(cfg, L, bits=4, group=128):
+    """Algorithmic HBM bytes of one batch-1 decode step of one LLaMA decoder layer: every packed
+    linear by SURVEY.md §8(d)'s formula (M = 1, fp16 scale + int8 zero per group) plus the K / V
+    cache rows the attention reads (L rows per KV head, fp16)."""
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    D = H // cfg.num_attention_heads
+    kv = cfg.num_key_value_heads * D
+    lin = [(H, H), (kv, H), (kv, H), (H, H), (I, H), (I, H), (H, I)]  # (N, K): q k v o gate up down
+    w = sum(algo_bytes(1, N, K, bits, group) for N, K in lin)
+    return w + 2 * cfg.num_key_value_heads * L * D * 2, sum(2 * N * K for N, K in lin)
+
+
+def decode_layer_bench(args, dev, timed):
+    """The product's decode path (BASELINE configs[1] inside the model): one batch-1 decode step
+    through R distinct LLaMA3-8B-shaped QuantLlamaDecoderLayers (hidden 4096, intermediate 14336,
+    32 / 8 heads; random N(0, 0.02^2) weights, RTN int4 g128, packed and fused with the KV cache
+    appended in place: five launches per layer), KV cache of --decode-kv rows, graph-replayed;
+    R * 114 MB of weights stream from HBM (beyond the 256 MB MALL).  The reference path it replaces
+    is QuantLlamaDecoderLayer.forward at q_len 1 (models/int_llama_layer.py:213-267, every
+    QuantLinear.forward = F.linear on W_dq, quant/int_linear.py:62)."""
+    import torch
+    from transformers import LlamaConfig
+    from models.int_llama_layer import QuantLlamaDecoderLayer
+    from models.quant_llama import quant_args, random_llama_layer, rtn_quantize_
+    R, kv = args.decode_layers, args.decode_kv
+    cfg = LlamaConfig(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
+                      num_key_value_heads=8, num_hidden_layers=R, vocab_size=128256,
+                      max_position_embeddings=8192, rms_norm_eps=1e-5, rope_theta=500000.0)
+    qa = quant_args(4, 128)
+
+    class Stack(torch.nn.Module):
+        def __init__(self, ls):
+            super().__init__()
+            self.layers = torch.nn.ModuleList(ls)
+    layers = []
+    for i in range(R):
+        st1 = Stack([QuantLlamaDecoderLayer(cfg, random_llama_layer(cfg, 100 + i, dev,
+                                                                    torch.float16), qa)])
+        rtn_quantize_(st1, pack=True)  # fp16 weights dropped per layer: only packed bytes stay
+        st1.layers[0].fuse_packed_projections(kv_cache=True)
+        layers.append(st1.layers[0])
+    g = torch.Generator(device=dev).manual_seed(0)
+    D = cfg.hidden_size // cfg.num_attention_heads
+    past = []
+    for layer in layers:
+        pk = (torch.randn(1, cfg.num_key_value_heads, kv, D, device=dev, dtype=torch.float16,
+                          generator=g),
+              torch.randn(1, cfg.num_key_value_heads, kv, D, device=dev, dtype=torch.float16,
+                          generator=g))
+        past.append(layer.self_attn.adopt_kv_cache(pk))
+    x = torch.randn(1, 1, cfg.hidden_size, device=dev, dtype=torch.float16, generator=g)
+    mask = torch.zeros(1, 1, 1, kv + 1, device=dev, dtype=torch.float16)
+    pos = torch.tensor([[kv]], device=dev)
+
+    def step():
+        h = x
+        for layer, pkv in zip(layers, past):
+            h = layer(h, attention_mask=mask, position_ids=pos, past_key_value=pkv,
+                      use_cache=True)[0]
+        return h
+
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s), torch.no_grad():
+        step()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph), torch.no_grad():
+        step()
+    steps = max(10, args.steps // 2)
+    el, _ = timed(graph.replay, steps, max(2, args.warmup // 2))
+    us = el / steps / R * 1e6
+    nbytes, flops = decode_layer_bytes(cfg, kv + 1)
+    out = {"workload": "decode_layer_int4_g128",
+           "what": ("LLaMA3-8B decoder layer, batch-1 decode step, int4 g128 packed + fused "
+                    "(q/k/v+RMSNorm, attention+RoPE+KV append, o+residual, gate/up+RMSNorm+SiLU*up, "
+                    "down+residual: 5 launches), graph-replayed over distinct layers"),
+           "layers": R, "kv_len": kv + 1, "us_per_layer": round(us, 2),
+           "est_32_layer_token_ms": round(us * 32 / 1e3, 3),
+           "tflops": round(flops / us / 1e6, 3),
+           "roofline": {"bound": "hbm", "achieved": round(nbytes / us / 1e3, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "bytes_per_layer": nbytes,
+                        "bytes": "7 packed linears by SURVEY §8(d) + the K / V rows read",
+                        "timing": "HIP events over graph replays / layers"}}
+    pmc = _pmc_traffic("decode_layer_int4_g128")
+    if pmc is not None:
+        out["roofline"]["traffic"] = round(pmc["fetch_bytes_per_launch"])
+        out["roofline"]["traffic_source"] = pmc["file"]
+    # the persistent one-launch engine over the same layers (opt-in; DESIGN.md §4)
+    if args.decode_engine:
+        from models.decode_engine import DecodeEngine
+        eng = DecodeEngine(layers)
+        if eng.reason is None:
+            with torch.no_grad():
+                eng_run = lambda: eng.step(x, pos, past, mask)  # noqa: E731
+                el_e, _ = timed(eng_run, steps, 2)
+            ue = el_e / steps / R * 1e6
+            out["engine"] = {"us_per_layer": round(ue, 2), "status": eng.status(),
+                             "frac": round(nbytes / ue / 1e3 / HBM_PEAK_GBS, 4)}
+    del graph, layers
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -383,6 +495,8 @@ def main():
     }
     if other is not None:
         out["other_mode"] = other
+    if kernel == "gemv" and args.workload == "gemv_int4_g128" and not args.no_decode_layer:
+        out["decode_layer"] = decode_layer_bench(args, dev, timed)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(M, N, K, bits, group, args.cpu_seconds) \
             if kernel != "gemm" else cpu_baseline(min(M, 32), N, K, bits, group, args.cpu_seconds)
