@@ -248,6 +248,7 @@ __device__ __forceinline__ bool wait_ready(Smem& sm, int seq) {
   const uint32_t xa = (uint32_t)(uintptr_t)(lds_int*)&sm.xready;
   const uint32_t aa = (uint32_t)(uintptr_t)(lds_int*)&sm.abort_;
   int ok, sv, cnt, v, w;
+  seq = __builtin_amdgcn_readfirstlane(seq);  // uniform: keep it in an SGPR for s_cmp
   asm volatile(
       "s_mov_b32 %[cnt], %[lim]\n"
       "1:\n\t"
