@@ -11,7 +11,14 @@ input), used by main.py:66-86 when a model does not fit one GPU.  Differences, b
     no tensor is reduced across stages;
   * rank 0 owns the embedding, the last rank owns the final norm + lm_head;
   * several windows (micro-batches) are kept in flight (GPipe-style fill): stage r computes
-    micro-batch i while stage r+1 computes micro-batch i-1; sends are asynchronous.
+    micro-batch i while stage r+1 computes micro-batch i-1; sends are asynchronous;
+  * decode (``generate``): greedy autoregressive decoding of several independent sequences
+    (micro-batches) — each stage keeps the KV cache of its own layers for every micro-batch
+    (the reference's per-layer ``past_key_value``, models/int_llama_layer.py:130-135, or the fused
+    layer's in-place cache buffers swapped in per micro-batch), the last stage picks each next
+    token and sends one [n_micro, B, 1] tensor back to the first stage per step.
+  * transport: RCCL point-to-point with ``nccl``; with ``gloo`` device tensors are staged through
+    host memory (gloo's send / recv take CPU tensors), e.g. several ranks sharing one GPU in tests.
 
 Stage outputs are bit-identical to the single-process model: each layer sees exactly the same
 input tensor, only on another device.
@@ -81,10 +88,37 @@ class PipelineRunner:
         self.dtype = dtype
         self.device = torch.device(device)
 
-    def _recv(self):
-        buf = torch.empty(self.hidden_shape, dtype=self.dtype, device=self.device)
-        dist.recv(buf, src=self.info.rank - 1)
+    def _host_staged(self):
+        return dist.get_backend() == "gloo" and self.device.type != "cpu"
+
+    def _recv(self, shape=None, dtype=None, src=None):
+        shape = self.hidden_shape if shape is None else tuple(shape)
+        dtype = self.dtype if dtype is None else dtype
+        src = self.info.rank - 1 if src is None else src
+        if self._host_staged():
+            buf = torch.empty(shape, dtype=dtype)
+            dist.recv(buf, src=src)
+            return buf.to(self.device)
+        buf = torch.empty(shape, dtype=dtype, device=self.device)
+        dist.recv(buf, src=src)
         return buf
+
+    def _bcast(self, t, src):
+        """broadcast in place (through host memory for gloo with device tensors)"""
+        if self._host_staged():
+            h = t.cpu()
+            dist.broadcast(h, src=src)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src=src)
+        return t
+
+    def _isend(self, t, dst):
+        """(request, the tensor kept alive until the request completes)"""
+        t = t.contiguous()
+        if self._host_staged():
+            t = t.cpu()
+        return dist.isend(t, dst=dst), t
 
     @torch.no_grad()
     def forward(self, micro_batches=None, n_micro=None):
@@ -109,11 +143,88 @@ class PipelineRunner:
             if info.last:
                 outs.append(self.model.head(h))
             else:
-                h = h.contiguous()
-                pending.append((dist.isend(h, dst=info.rank + 1), h))
+                pending.append(self._isend(h, info.rank + 1))
         for req, _ in pending:
             req.wait()
         return outs if info.last else None
+
+    # -- decode ----------------------------------------------------------------------------------
+    def _layers_step(self, h, mb, pos0):
+        """This stage's layers over h [B, T, H] of micro-batch ``mb`` at positions pos0..pos0+T-1,
+        with that micro-batch's own KV cache per layer: the ``past_key_value`` each layer returned
+        last time, and for layers in kv_cache mode (fuse_packed_projections(kv_cache=True)) their
+        cache buffers, swapped in so the append stays in place."""
+        B, T = h.shape[:2]
+        from .quant_llama import causal_mask
+        mask = causal_mask(B, T, h.dtype, h.device, past=pos0)
+        pos = torch.arange(pos0, pos0 + T, device=h.device)[None].expand(B, T)
+        n = len(self.model.layers)
+        past = self._past.setdefault(mb, [None] * n)
+        bufs = self._bufs.setdefault(mb, [None] * n)
+        for j, layer in enumerate(self.model.layers):
+            at = layer.self_attn
+            own = bool(getattr(at, "kv_cache", False))
+            if own:
+                at._kv = bufs[j]
+            h, past[j] = layer(h, attention_mask=mask, position_ids=pos, past_key_value=past[j],
+                               use_cache=True)
+            if own:
+                bufs[j] = at._kv
+        return h
+
+    @torch.no_grad()
+    def generate(self, prompts=None, n_new=8):
+        """Greedy decoding of independent sequences through the pipeline.  ``prompts``: list of
+        int64 token tensors [B, T] (one micro-batch each, same shape), needed on the first stage
+        only.  Step 0 runs the prompts (prefill) and picks the first new token; each later step
+        runs one token per sequence over the stages' KV caches.  Returns int64 [n_micro, B, n_new]
+        on every rank."""
+        info = self.info
+        multi = info.world > 1
+        meta = torch.zeros(3, dtype=torch.int64)
+        if info.first:
+            if not prompts:
+                raise ValueError("the first stage needs the prompts")
+            shapes = {tuple(p.shape) for p in prompts}
+            if len(shapes) != 1 or len(next(iter(shapes))) != 2:
+                raise ValueError("prompts must share one [B, T] shape")
+            meta = torch.tensor([len(prompts), *prompts[0].shape], dtype=torch.int64)
+        if multi:
+            meta = self._bcast(meta.to(self.device), 0).cpu()
+        n_micro, B, T = (int(v) for v in meta.tolist())
+        H = self.hidden_shape[-1]
+        self._past, self._bufs = {}, {}
+        out = torch.zeros(n_micro, B, n_new, dtype=torch.int64, device=self.device)
+        cur = None  # [n_micro, B, 1] next input tokens (first stage)
+        for step in range(n_new):
+            T_in, pos0 = (T, 0) if step == 0 else (1, T + step - 1)
+            pending, nxt = [], []
+            for i in range(n_micro):
+                if info.first:
+                    ids = prompts[i].to(self.device) if step == 0 else cur[i]
+                    h = self.model.embed_tokens(ids)
+                else:
+                    h = self._recv((B, T_in, H))
+                h = self._layers_step(h, i, pos0)
+                if info.last:
+                    nxt.append(self.model.head(h[:, -1:]).argmax(-1))  # [B, 1]
+                else:
+                    pending.append(self._isend(h, info.rank + 1))
+            for req, _ in pending:
+                req.wait()
+            if info.last:
+                tok = torch.stack(nxt)  # [n_micro, B, 1]
+                out[:, :, step] = tok[:, :, 0]
+                if info.first:
+                    cur = tok
+                elif step + 1 < n_new:
+                    req, keep = self._isend(tok, 0)
+                    req.wait()
+            elif info.first and step + 1 < n_new:
+                cur = self._recv((n_micro, B, 1), torch.int64, src=info.world - 1)
+        if multi:
+            self._bcast(out, info.world - 1)
+        return out
 
     @torch.no_grad()
     def window_nlls(self, windows):
@@ -121,7 +232,7 @@ class PipelineRunner:
         ranks, so every rank can form the perplexity."""
         n = len(windows) if windows is not None else None
         n_t = torch.tensor([n if n is not None else 0], dtype=torch.int64, device=self.device)
-        dist.broadcast(n_t, src=0)
+        self._bcast(n_t, 0)
         n = int(n_t.item())
         logits = self.forward(windows if self.info.first else None, n_micro=n)
         from .quant_llama import nll_from_logits
@@ -133,20 +244,30 @@ class PipelineRunner:
                 nll[i] = nll_from_logits(lg, labels[i])
         elif self.info.first:
             self._send_labels(windows)
-        dist.broadcast(nll, src=self.info.world - 1)
+        self._bcast(nll, self.info.world - 1)
         return nll
 
     def _send_labels(self, windows):
         for w in windows:
-            dist.send(w.to(self.device).contiguous(), dst=self.info.world - 1)
+            req, _ = self._isend(w.to(self.device), self.info.world - 1)
+            req.wait()
 
     def _labels_from_first(self, n):
         out = []
         for _ in range(n):
-            buf = torch.empty(self.hidden_shape[:2], dtype=torch.int64, device=self.device)
-            dist.recv(buf, src=0)
-            out.append(buf)
+            out.append(self._recv(self.hidden_shape[:2], torch.int64, src=0))
         return out
+
+
+@torch.no_grad()
+def greedy_generate(model, prompts, n_new):
+    """The same greedy decoding in one process (world size 1): the reference's loop of
+    QuantLlamaDecoderLayer.forward with use_cache=True over a prompt, then one token at a time."""
+    info = StageInfo(0, 1, 0, len(model.layers))
+    H = model.config.hidden_size
+    runner = PipelineRunner(model, info, (1, 1, H), model.embed_tokens.weight.dtype,
+                            model.embed_tokens.weight.device)
+    return runner.generate(prompts, n_new)
 
 
 def single_stage_nlls(model, windows):

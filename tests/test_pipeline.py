@@ -1,10 +1,12 @@
-"""Pipeline sharding of the decoder stack (models/pipeline.py) on CPU with gloo, world size 2 and
-3: logits and per-window NLL must equal the single-process model bit for bit (no cross-stage
-reduction exists), and the stage split must cover every layer exactly once.
+"""Pipeline sharding of the decoder stack (models/pipeline.py) with gloo, world size 2 and 3:
+logits, per-window NLL and greedy decoding (the decode micro-batch mode: per-stage KV caches per
+sequence) must equal the single-process model bit for bit (no cross-stage reduction exists), and
+the stage split must cover every layer exactly once.
 
-The layers run unquantized here (QuantLinear with quant state off -> F.linear), which keeps the
-test on CPU: what is under test is the stage orchestration and the send/recv plumbing, the same
-code the GPU run drives over RCCL."""
+CPU tests: the layers run unquantized (QuantLinear with quant state off -> F.linear), so what is
+under test is the stage orchestration and the send/recv plumbing, the same code the GPU run drives
+over RCCL.  GPU test: both ranks on cuda:0 (gloo, hand-offs staged through host memory), every
+stage running packed int4 layers through the gfx950 kernels, fused with the in-place KV cache."""
 import os
 import socket
 
@@ -13,8 +15,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from models.pipeline import PipelineRunner, stage_bounds, stage_info
-from models.quant_llama import build_random_quant_llama, quant_args, window_nll
+from models.pipeline import PipelineRunner, greedy_generate, stage_bounds, stage_info
+from models.quant_llama import build_random_quant_llama, quant_args, rtn_quantize_, window_nll
 
 N_LAYERS = 5
 T = 12
@@ -28,9 +30,16 @@ def _cfg():
                        max_position_embeddings=64, rms_norm_eps=1e-5, rope_theta=500000.0)
 
 
-def _windows():
+def _windows(vocab=101):
     g = torch.Generator().manual_seed(7)
-    return [torch.randint(0, 101, (1, T), generator=g) for _ in range(N_WIN)]
+    return [torch.randint(0, vocab, (1, T), generator=g) for _ in range(N_WIN)]
+
+
+def _gpu_cfg():
+    from transformers import LlamaConfig
+    return LlamaConfig(hidden_size=512, intermediate_size=1408, num_attention_heads=4,
+                       num_key_value_heads=2, num_hidden_layers=4, vocab_size=1000,
+                       max_position_embeddings=256, rms_norm_eps=1e-5, rope_theta=500000.0)
 
 
 def _free_port():
@@ -39,21 +48,52 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _prompts(vocab, n=2, B=1, T_=5, seed=8):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randint(0, vocab, (B, T_), generator=g) for _ in range(n)]
+
+
+def _packed_model(cfg, device, layer_ids=None):
+    """int4 g128 RTN, packed, fused with the in-place KV cache (the decode product path)."""
+    model = build_random_quant_llama(cfg, quant_args(4, 128), seed=4, device=device,
+                                     dtype=torch.float16, layer_ids=layer_ids)
+    rtn_quantize_(model, pack=True)
+    for layer in model.layers:
+        layer.fuse_packed_projections(kv_cache=True)
+    return model
+
+
+N_NEW = 4
+
+
+def _worker(rank, world, port, out_dir, gpu=False):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     try:
         torch.manual_seed(0)
-        cfg = _cfg()
-        info = stage_info(N_LAYERS, rank, world)
-        model = build_random_quant_llama(cfg, quant_args(wbits=16), seed=3, device="cpu",
-                                         dtype=torch.float32,
-                                         layer_ids=range(info.lo, info.hi))
-        runner = PipelineRunner(model, info, (1, T, cfg.hidden_size), torch.float32, "cpu")
-        wins = _windows() if info.first else None
+        if gpu:
+            cfg = _gpu_cfg()
+            info = stage_info(cfg.num_hidden_layers, rank, world)
+            dev = torch.device("cuda", 0)
+            model = _packed_model(cfg, dev, layer_ids=range(info.lo, info.hi))
+            runner = PipelineRunner(model, info, (1, T, cfg.hidden_size), torch.float16, dev)
+            wins = [w.to(dev) for w in _windows(cfg.vocab_size)] if info.first else None
+            dtype_dev = dev
+        else:
+            cfg = _cfg()
+            info = stage_info(N_LAYERS, rank, world)
+            model = build_random_quant_llama(cfg, quant_args(wbits=16), seed=3, device="cpu",
+                                             dtype=torch.float32,
+                                             layer_ids=range(info.lo, info.hi))
+            runner = PipelineRunner(model, info, (1, T, cfg.hidden_size), torch.float32, "cpu")
+            wins = _windows() if info.first else None
+            dtype_dev = "cpu"
         logits = runner.forward(wins, n_micro=N_WIN)
         nll = runner.window_nlls(wins)
-        torch.save({"logits": logits, "nll": nll, "lo": info.lo, "hi": info.hi},
+        prompts = [p.to(dtype_dev) for p in _prompts(cfg.vocab_size)] if info.first else None
+        toks = runner.generate(prompts, N_NEW)
+        torch.save({"logits": None if logits is None else [x.cpu() for x in logits],
+                    "nll": nll.cpu(), "tokens": toks.cpu(), "lo": info.lo, "hi": info.hi},
                    os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
         # every rank past its last collective before any tears gloo down (a rank destroying its
@@ -83,18 +123,57 @@ def test_pipeline_matches_single_process(tmp_path, world):
     with torch.no_grad():
         ref_logits = [full(w) for w in wins]
         ref_nll = torch.stack([window_nll(full, w) for w in wins])
+    ref_tok = greedy_generate(full, _prompts(cfg.vocab_size), N_NEW)
+    _check_pipeline(tmp_path, world, N_LAYERS, ref_logits, ref_nll, ref_tok, gpu=False)
 
+
+def _check_pipeline(tmp_path, world, n_layers, ref_logits, ref_nll, ref_tok, gpu):
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, port, str(tmp_path), gpu), nprocs=world, join=True,
                        start_method="spawn")
     outs = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True)
             for r in range(world)]
-    assert [o["lo"] for o in outs] == [b[0] for b in stage_bounds(N_LAYERS, world)]
+    assert [o["lo"] for o in outs] == [b[0] for b in stage_bounds(n_layers, world)]
     last = outs[-1]
     assert len(last["logits"]) == N_WIN
     for got, ref in zip(last["logits"], ref_logits):
-        assert torch.equal(got, ref)  # bit-identical: same ops on the same tensors
-    for o in outs:  # every rank received the broadcast NLLs
-        assert torch.equal(o["nll"], ref_nll.to(o["nll"].dtype))
+        assert torch.equal(got, ref.cpu())  # bit-identical: same ops on the same tensors
+    for o in outs:  # every rank received the broadcast NLLs and the generated tokens
+        assert torch.equal(o["nll"], ref_nll.cpu().to(o["nll"].dtype))
+        assert torch.equal(o["tokens"], ref_tok.cpu())
     for o in outs[:-1]:
         assert o["logits"] is None
+
+
+def test_greedy_generate_uses_the_kv_cache():
+    """The decode path (prefill + cached one-token steps) picks the same tokens as re-running the
+    whole growing sequence without a cache."""
+    cfg = _cfg()
+    full = build_random_quant_llama(cfg, quant_args(wbits=16), seed=3, device="cpu",
+                                    dtype=torch.float32)
+    prompts = _prompts(cfg.vocab_size, n=2, B=2)
+    got = greedy_generate(full, prompts, N_NEW)
+    assert got.shape == (2, 2, N_NEW)
+    with torch.no_grad():
+        for i, p in enumerate(prompts):
+            seq = p
+            for s in range(N_NEW):
+                nxt = full(seq)[:, -1].argmax(-1, keepdim=True)
+                assert torch.equal(nxt[:, 0], got[i, :, s])
+                seq = torch.cat([seq, nxt], 1)
+
+
+@pytest.mark.gpu
+def test_pipeline_packed_stages_on_gpu(tmp_path):
+    """World 2 on one MI355X (gloo, host-staged hand-offs): each stage runs packed int4 layers
+    through the gfx950 kernels (fused, in-place KV cache in decode) — logits, NLL and greedy
+    tokens equal the single-process packed model bit for bit."""
+    cfg = _gpu_cfg()
+    dev = torch.device("cuda", 0)
+    full = _packed_model(cfg, dev)
+    wins = [w.to(dev) for w in _windows(cfg.vocab_size)]
+    with torch.no_grad():
+        ref_logits = [full(w) for w in wins]
+        ref_nll = torch.stack([window_nll(full, w) for w in wins])
+    ref_tok = greedy_generate(full, [p.to(dev) for p in _prompts(cfg.vocab_size)], N_NEW)
+    _check_pipeline(tmp_path, 2, cfg.num_hidden_layers, ref_logits, ref_nll, ref_tok, gpu=True)

@@ -38,6 +38,11 @@ def main():
     ap.add_argument("--fake-quant", action="store_true", help="dense F.linear on W_dq instead of packed")
     ap.add_argument("--fused", action="store_true",
                     help="packed + fuse_packed_projections() (fused q/k/v, gate/up+SiLU, epilogues)")
+    ap.add_argument("--decode", type=int, default=0,
+                    help="also greedy-decode this many tokens for --micro sequences (decode "
+                         "micro-batch mode: per-stage KV caches; fused layers use kv_cache=True)")
+    ap.add_argument("--micro", type=int, default=0, help="decode sequences (default: world size)")
+    ap.add_argument("--prompt", type=int, default=128, help="decode prompt length")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -56,7 +61,7 @@ def main():
     rtn_quantize_(model, pack=not a.fake_quant)
     if a.fused and not a.fake_quant:
         for layer in model.layers:
-            layer.fuse_packed_projections()
+            layer.fuse_packed_projections(kv_cache=a.decode > 0)
     g = torch.Generator(device=dev).manual_seed(123)
     wins = [torch.randint(0, a.vocab, (1, a.tokens), device=dev, generator=g)
             for _ in range(a.windows)] if info.first else None
@@ -69,6 +74,24 @@ def main():
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
+    dec = None
+    if a.decode > 0:
+        n_micro = a.micro or world
+        prompts = [torch.randint(0, a.vocab, (1, a.prompt), device=dev, generator=g)
+                   for _ in range(n_micro)] if info.first else None
+        dr = PipelineRunner(model, info, (1, 1, a.hidden), torch.float16, dev)
+        dr.generate(prompts, 2)  # warm
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        toks = dr.generate(prompts, a.decode)
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt_dec = time.perf_counter() - t1
+        dec = {"sequences": n_micro, "prompt": a.prompt, "new_tokens": a.decode,
+               "ms_per_step": round(dt_dec / a.decode * 1e3, 3),
+               "tokens_per_s": round(n_micro * a.decode / dt_dec, 1),
+               "first_tokens": toks[:, 0, :8].tolist()}
     if rank == 0:
         ppl = float(torch.exp(nll.sum() / (a.windows * a.tokens)))
         print(json.dumps({"world": world, "layers": a.layers, "stages": [list(x) for x in
@@ -77,7 +100,7 @@ def main():
                           f"packed{' fused' if a.fused else ''} int{a.wbits} g{a.group}",
                           "windows": a.windows, "tokens": a.tokens, "ppl": ppl,
                           "ms_per_window": round(dt / a.windows * 1e3, 2),
-                          "nll": [round(float(v), 4) for v in nll]}))
+                          "nll": [round(float(v), 4) for v in nll], "decode": dec}))
     dist.barrier()  # no rank tears its transport down while a peer is still draining
     dist.destroy_process_group()
 
