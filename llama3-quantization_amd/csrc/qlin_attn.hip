@@ -42,8 +42,8 @@ constexpr int kMaxL = 4096;
 constexpr int kSub = 64;         // positions per pass (8 lanes x 16 dims per K row)
 constexpr int kMaxChunk = 512;   // scores of one chunk live in LDS: 512 x 8 fp32 = 16 KB
 constexpr int kMaxSplit = kMaxL / kSub;
-#ifndef ATTN_TARGET_BLOCKS  // dev sweeps (tools/dev/Makefile libattnT<N>.so)
-#define ATTN_TARGET_BLOCKS 1024
+#ifndef ATTN_TARGET_BLOCKS  // dev sweeps (tools/dev/Makefile libattnT<N>.so); round 3: 256
+#define ATTN_TARGET_BLOCKS 256   // (tools/dev/attn_ab.py: L = 4096 17.2 -> 14.7 us, L <= 2048 +-0)
 #endif
 constexpr int kTargetBlocks = ATTN_TARGET_BLOCKS;
 
@@ -343,7 +343,19 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   __threadfence();
 #endif
 
-  // merge: chunk statistics -> weights exp(m_s - M) and denominators sum_s w_s l_s
+  // merge: the first kPre partial rows of every wave (s = wave + 4 i) are requested together with
+  // the chunk statistics — one memory round trip instead of two at decode lengths (S <= 16)
+  constexpr int J = GRP * kD / 64;
+  constexpr int kPre = GRP <= 4 ? 4 : 2;
+  const float* pb = part_o + (int64_t)bh * S * GRP * kD + lane;
+  float xpre[kPre][J];
+#pragma unroll
+  for (int i = 0; i < kPre; ++i) {
+    const int s = min(wave + kWaves * i, S - 1);
+#pragma unroll
+    for (int j = 0; j < J; ++j) xpre[i][j] = part_load(pb + (int64_t)s * GRP * kD + 64 * j);
+  }
+  // chunk statistics -> weights exp(m_s - M) and denominators sum_s w_s l_s
   const float* mlb = part_ml + (int64_t)bh * S * GRP * 2;
   for (int i = tid; i < S * GRP; i += kThreads) {
     mw[i / GRP][i % GRP] = part_load(mlb + 2 * i);
@@ -367,17 +379,36 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   // weighted sum of the S partial rows: wave w takes rows s = w, w + 4, ...; lane owns floats
   // o = lane + 64 j of the GRP x 128 row (one coalesced 256-B load per wave and j)
   {
-    constexpr int J = GRP * kD / 64;
     float acc[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[j] = 0.f;
-    const float* pb = part_o + (int64_t)bh * S * GRP * kD + lane;
-    for (int s = wave; s < S; s += kWaves) {
-      float x[J];
+    // rows s = wave + 4 i, i < kPre, arrived with the statistics (same order as the loop below)
 #pragma unroll
-      for (int j = 0; j < J; ++j) x[j] = part_load(pb + (int64_t)s * GRP * kD + 64 * j);
+    for (int i = 0; i < kPre; ++i) {
+      const int s = wave + kWaves * i;
+      if (s < S) {
 #pragma unroll
-      for (int j = 0; j < J; ++j) acc[j] = fmaf(mw[s][(64 * j + lane) / kD], x[j], acc[j]);
+        for (int j = 0; j < J; ++j) acc[j] = fmaf(mw[s][(64 * j + lane) / kD], xpre[i][j], acc[j]);
+      }
+    }
+    // the rest in rounds of kPre rows, every load of a round issued before its FMAs (long caches:
+    // S = 64 at L = 4096 was 16 dependent round trips per wave)
+    for (int s0 = wave + kWaves * kPre; s0 < S; s0 += kWaves * kPre) {
+      float x[kPre][J];
+#pragma unroll
+      for (int i = 0; i < kPre; ++i) {
+        const int s = min(s0 + kWaves * i, S - 1);
+#pragma unroll
+        for (int j = 0; j < J; ++j) x[i][j] = part_load(pb + (int64_t)s * GRP * kD + 64 * j);
+      }
+#pragma unroll
+      for (int i = 0; i < kPre; ++i) {
+        const int s = s0 + kWaves * i;
+        if (s < S) {
+#pragma unroll
+          for (int j = 0; j < J; ++j) acc[j] = fmaf(mw[s][(64 * j + lane) / kD], x[i][j], acc[j]);
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) po[wave][lane + 64 * j] = acc[j];

@@ -353,6 +353,9 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
 #ifndef GEMV_NRM_XFIRST  // dev switch: the fused norm's x words issued before the codes
 #define GEMV_NRM_XFIRST 1
 #endif
+#ifndef GEMV_NRM_ABLATE  // dev ablation (wrong results): 1 = no in-kernel statistics (constant
+#define GEMV_NRM_ABLATE 0  // rsqrt, no barrier): the upper bound of precomputed statistics
+#endif
 struct FastArgs {
   const uint32_t* qw;   // row tile 0 of qweight
   const uint32_t* qsz;  // row tile 0 of qsz
@@ -465,7 +468,9 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   if constexpr (EP == kEpResidual) ores = a.res[(int64_t)om * a.N + min(orow, (int64_t)a.N - 1)];
 
   float rn = 1.f;  // NRM: rsqrt(mean(x^2) + eps)
-  if constexpr (NRM) {
+  if constexpr (NRM && GEMV_NRM_ABLATE) {
+    rn = rsqrtf(1.f + a.eps);
+  } else if constexpr (NRM) {
 #pragma clang fp contract(off)
     float ss = 0.f;
 #pragma unroll
