@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 7
+#define QLIN_ABI_VERSION 8
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -232,11 +232,38 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
  * qlin_rmsnorm_linear_supported() says so (1) or not (0); otherwise QLIN_EINVAL.
  */
 int qlin_rmsnorm_linear_supported(int64_t M, int64_t N, int64_t K, int bits, int group);
+/*
+ * qlin_rmsnorm_linear_ep_f16 optional inputs (ABI 8), for the decode chain of a fused layer:
+ *   sumsq_in / sumsq_n  precomputed statistics: sumsq_n == ceil(K / 16) partial sums of squares
+ *                       of x, one per 16 consecutive elements, as qlin_linear_res_sumsq_f16 writes
+ *                       them while producing x; the norm then uses sum(partials) / K (a fixed
+ *                       order, the same in every block) instead of reducing x in every block
+ *                       behind a barrier.  NULL: computed in the kernel.  K <= 8192.
+ *   rope_pos / rope_cos / rope_sin / rope_rows / rope_out  copy the RoPE cos and sin rows of
+ *                       position rope_pos[0] (clamped to [0, rope_rows)) of the fp32 caches
+ *                       [rope_rows][128] into rope_out[0..127] / [128..255] (16-B aligned), for a
+ *                       following qlin_attn_decode_rope with position_ids NULL.  NULL: skipped.
+ */
 int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                                const uint16_t* x, const float* norm_weight, float eps,
                                const uint16_t* bias, const uint16_t* residual, uint16_t* y,
                                int64_t M, int64_t N, int64_t K, int bits, int group, int epilogue,
-                               void* stream);
+                               const float* sumsq_in, int64_t sumsq_n, const int64_t* rope_pos,
+                               const float* rope_cos, const float* rope_sin, int64_t rope_rows,
+                               float* rope_out, void* stream);
+
+/*
+ * One token row: y[N] = RN16(residual + RN16(x @ W_dq^T + bias)) (QLIN_EP_RESIDUAL of
+ * qlin_linear_ep_f16: o_proj / down_proj + the residual add, models/int_llama_layer.py:241-257)
+ * that also writes sumsq_out[ceil(N / 16)]: per 16 consecutive outputs, the sum of the squares of
+ * their fp16 values (fixed order) — the statistics of the RMSNorm that reads y next
+ * (post_attention_layernorm / the next layer's input_layernorm, quant/omni_norm.py:52-63), for
+ * qlin_rmsnorm_linear_ep_f16's sumsq_in.
+ */
+int qlin_linear_res_sumsq_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                              const uint16_t* x, const uint16_t* bias, const uint16_t* residual,
+                              uint16_t* y, int64_t N, int64_t K, int bits, int group,
+                              float* sumsq_out, void* stream);
 
 /*
  * Fused decode attention (one query token per sequence), for the quantized LLaMA layer's
@@ -268,7 +295,9 @@ int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const
  * qlin_rope_f16; the caches fp16 [B, Hkv, rows, D] with head stride kv_head_stride (>= L * D)
  * hold rows 0 .. L - 2 and receive the rotated k and the v row at L - 1 from this launch, which
  * then attends over all L rows (mask fp16 [B, L] or NULL).  Same arithmetic as the two launches
- * (bit-identical output and cache rows); partials / counters as qlin_attn_decode.
+ * (bit-identical output and cache rows); partials / counters as qlin_attn_decode.  B == 1 may
+ * pass position_ids NULL with cos / sin pointing at the step's own rows (e.g. the rope_out of
+ * the q/k/v launch, qlin_rmsnorm_linear_ep_f16): no position -> row round trip in this launch.
  */
 int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
                           int64_t k_row_stride, const uint16_t* v, int64_t v_row_stride,

@@ -168,7 +168,9 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   const bool has_new = ROPE && split == S - 1;  // this block's chunk holds the new row L - 1
   if constexpr (ROPE) {
 #pragma clang fp contract(off)
-    const int64_t p = min(max(ri.pos[(int64_t)b * ri.pos_bs], (int64_t)0), ri.cache_rows - 1);
+    // pos NULL: cosc / sinc already are the step's rows (qlin_rmsnorm_linear_ep_f16 rope_out)
+    const int64_t p =
+        ri.pos ? min(max(ri.pos[(int64_t)b * ri.pos_bs], (int64_t)0), ri.cache_rows - 1) : 0;
     const float* cr = ri.cosc + p * kD;
     const float* sr = ri.sinc + p * kD;
     constexpr int half = kD / 2;
@@ -493,7 +495,9 @@ extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, co
                                      const uint16_t* mask, void* out, int out_dtype, int64_t B,
                                      int Hq, int Hkv, int64_t L, int D, float scale_div,
                                      float* partials, int32_t* counters, void* stream) {
-  if (!q || !k || !v || !cos_cache || !sin_cache || !position_ids || !k_cache || !v_cache ||
+  // position_ids NULL: cos_cache / sin_cache are the rows of the step's position (B == 1)
+  if (!position_ids && B > 1) return QLIN_EINVAL;
+  if (!q || !k || !v || !cos_cache || !sin_cache || !k_cache || !v_cache ||
       !out || (out_dtype != QLIN_F32 && out_dtype != QLIN_F16) || B < 0 || Hq <= 0 ||
       Hkv <= 0 || Hq % Hkv || L <= 0 || L > kMaxL || D != kD || B * Hkv > 0x7fffffff ||
       q_row_stride < (int64_t)Hq * kD || k_row_stride < (int64_t)Hkv * kD ||

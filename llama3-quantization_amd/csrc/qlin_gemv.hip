@@ -52,6 +52,7 @@ struct Ep {  // output epilogue (qlin_common.h kEp*) and fused activation fake-q
   const uint16_t* res;
   int ep;
   ActQ aq;
+  float* sq_out = nullptr;  // M == 1, kEpResidual: per-tile sums of squares of y
 };
 
 struct Geo {
@@ -200,12 +201,24 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
 
 }
 
+// the sum of squares of the 16 outputs one tile row's block writes (lanes 0..15 of wave 0 hold
+// them; every other lane 0) in a fixed butterfly order -> sq_out[nt]: the statistics of the
+// RMSNorm that reads this output next (qlin_rmsnorm_linear_ep_f16's sumsq_in), precomputed
+__device__ __forceinline__ void sq_tile_out(float v, float* sq_out, int64_t nt) {
+#pragma clang fp contract(off)
+  v = v + __shfl_xor(v, 8);
+  v = v + __shfl_xor(v, 4);
+  v = v + __shfl_xor(v, 2);
+  v = v + __shfl_xor(v, 1);
+  if ((threadIdx.x & 63) == 0) sq_out[nt] = v;
+}
+
 template <int BITS, int MT, int GPT, int ZM, int PF, int NTB = 1>
 __global__ __launch_bounds__(1024) void gemv_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
     int M, int N, int K, int group, uint32_t gmagic, int tpw, const _Float16* __restrict__ res,
-    int ep, ActQ aq) {
+    int ep, ActQ aq, float* __restrict__ sq_out) {
   __shared__ __attribute__((aligned(16))) float red[NTB * MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
   __shared__ float aq_s[2][MT];
@@ -324,6 +337,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
     }
     return;
   }
+  float sqv = 0.f;  // sq_out: this thread's output squared
   for (int o = tid; o < NTB * MT * kTileN; o += blockDim.x) {
     const int j = o / (MT * kTileN), oo = o - j * MT * kTileN;
     const int m = oo / kTileN, n = oo - m * kTileN;
@@ -332,8 +346,11 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
       float t = total(o, row);
       if (ep == kEpResidual) t += (float)res[(int64_t)m * N + row];
       y[(int64_t)m * N + row] = (_Float16)t;
+      const float f = (float)(_Float16)t;
+      sqv = f * f;
     }
   }
+  if (sq_out && wave == 0) sq_tile_out(sqv, sq_out, nt);  // M == 1, NTB == 1 (host)
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -353,9 +370,23 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
 #ifndef GEMV_NRM_XFIRST  // dev switch: the fused norm's x words issued before the codes
 #define GEMV_NRM_XFIRST 1
 #endif
+#ifndef GEMV_NRM_LATE  // 1: the norm's rsqrt applied to the accumulators in the epilogue (x words
+#define GEMV_NRM_LATE 0  // rounded as RN16(w * x)): the first MFMAs wait for no statistics
+#endif
 #ifndef GEMV_NRM_ABLATE  // dev ablation (wrong results): 1 = no in-kernel statistics (constant
 #define GEMV_NRM_ABLATE 0  // rsqrt, no barrier): the upper bound of precomputed statistics
 #endif
+// qlin_rmsnorm_linear_ep_f16's optional inputs (precomputed statistics, RoPE row gather)
+struct NormIn {
+  const float* sq_in;
+  int sq_n;
+  const int64_t* rope_pos;
+  const float* rope_cos;
+  const float* rope_sin;
+  int64_t rope_rows;
+  float* rope_out;
+};
+
 struct FastArgs {
   const uint32_t* qw;   // row tile 0 of qweight
   const uint32_t* qsz;  // row tile 0 of qsz
@@ -368,7 +399,16 @@ struct FastArgs {
   uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
   const float* nw;      // NRM: RMSNorm weight (fp32 [K]) applied to x first
   float eps;
+  const float* sq_in;   // NRM: precomputed statistics (sq_n partial sums of squares of x), or null
+  int sq_n;
+  float* sq_out;        // EP == kEpResidual, M == 1: per-tile sums of squares of y, or null
+  const int64_t* rope_pos;  // block 0, wave 0: copy cos / sin row rope_pos[0] to rope_out
+  const float* rope_cos;
+  const float* rope_sin;
+  int64_t rope_rows;
+  float* rope_out;      // [2][128] fp32, or null
 };
+constexpr int kSqMaxPerLane = 8;  // sumsq_in partials per lane (K <= 64 * 8 * 16 = 8192)
 
 // every wave streams at most PF tiles, all of them loaded up front (no refill loop: a launch whose
 // waves need more tiles takes gemv_kernel, whose contiguous tile runs stream better then).
@@ -400,6 +440,22 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   const int nts = (a.Kt - wave + a.W - 1) >> a.lw;  // >= 1: W <= Kt
   const int ktl = wave + ((nts - 1) << a.lw);        // the wave's last tile
 
+  // precomputed norm statistics: issued before every other load (in-order completion: the norm
+  // then waits for these alone, not for the weights)
+  float sqp[NRM ? kSqMaxPerLane : 1];
+  if constexpr (NRM) {
+    if (a.sq_in) {
+#pragma unroll
+      for (int i = 0; i < kSqMaxPerLane; ++i) sqp[i] = a.sq_in[min(lane + 64 * i, a.sq_n - 1)];
+    }
+  }
+  if (a.rope_out && nt == 0 && wave == 0) {
+    // the step's RoPE cos / sin row for the attention launch that follows (it then skips the
+    // position -> row round trip); tiny, and only block 0's wave 0 pays it
+    const int64_t p = min(max(a.rope_pos[0], (int64_t)0), a.rope_rows - 1);
+    const float* src = (lane < 32 ? a.rope_cos : a.rope_sin) + p * 128 + 4 * (lane & 31);
+    *reinterpret_cast<float4*>(a.rope_out + 4 * lane) = *reinterpret_cast<const float4*>(src);
+  }
   auto kt_of = [&](int i) { return min(wave + (i << a.lw), ktl); };
   auto group_of_tile = [&](int kt) {
     return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
@@ -468,9 +524,32 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   if constexpr (EP == kEpResidual) ores = a.res[(int64_t)om * a.N + min(orow, (int64_t)a.N - 1)];
 
   float rn = 1.f;  // NRM: rsqrt(mean(x^2) + eps)
-  if constexpr (NRM && GEMV_NRM_ABLATE) {
+  float ss_late = 0.f;  // GEMV_NRM_LATE: this wave's sum of squares of its x words
+  if constexpr (NRM && GEMV_NRM_LATE) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (u < nts) {
+        const h2 v = as_h2(xq[u].w[0]);
+        const float f0 = (float)v.x, f1 = (float)v.y;
+        ss_late = ss_late + f0 * f0;
+        ss_late = ss_late + f1 * f1;
+      }
+    }
+  } else if constexpr (NRM && GEMV_NRM_ABLATE) {
     rn = rsqrtf(1.f + a.eps);
   } else if constexpr (NRM) {
+   if (a.sq_in) {
+#pragma clang fp contract(off)
+    // sum of partial i over i = lane + 64 j (j in order), then the wave butterfly: the same
+    // order in every wave and block, and no barrier
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSqMaxPerLane; ++i)
+      if (lane + 64 * i < a.sq_n) ss = ss + sqp[i];
+    ss = wave_sum(ss);
+    rn = rsqrtf(ss / (float)a.K + a.eps);
+   } else {
 #pragma clang fp contract(off)
     float ss = 0.f;
 #pragma unroll
@@ -490,6 +569,7 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
     float tot = 0.f;
     for (int w = 0; w < a.W; ++w) tot += nss[w];
     rn = rsqrtf(tot / (float)a.K + a.eps);
+   }
   }
 
   const Magics mg = make_magics<BITS>();
@@ -500,7 +580,8 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
     if constexpr (NRM) {
 #pragma clang fp contract(off)
       const h2 v = as_h2(xq[u].w[0]);
-      const float n0 = nwv[u].x * ((float)v.x * rn), n1 = nwv[u].y * ((float)v.y * rn);
+      const float n0 = GEMV_NRM_LATE ? nwv[u].x * (float)v.x : nwv[u].x * ((float)v.x * rn);
+      const float n1 = GEMV_NRM_LATE ? nwv[u].y * (float)v.y : nwv[u].y * ((float)v.y * rn);
       xq[u].w[0] = as_u32(h2{(_Float16)n0, (_Float16)n1});
     }
     park_x<MT>(xa, xq[u], slot, lane, n_in);
@@ -541,15 +622,26 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
 #pragma unroll
         for (int e = 0; e < 4 && e < MT; ++e) red[((q4 + e) * kTileN + n_in) * kMaxWaves + w] = 0.f;
   }
+  if constexpr (NRM && GEMV_NRM_LATE) {
+    const float ssw = wave_sum(ss_late);
+    if (lane == 0) nss[wave] = ssw;
+  }
   __syncthreads();
+  if constexpr (NRM && GEMV_NRM_LATE) {
+    float tot = 0.f;
+    for (int w = 0; w < a.W; ++w) tot += nss[w];
+    rn = rsqrtf(tot / (float)a.K + a.eps);
+  }
   auto total = [&](int o, _Float16 b) {
     const f4* r = reinterpret_cast<const f4*>(red + o * kMaxWaves);
     const f4 p = r[0], q = r[1], c = r[2], d = r[3];
     const f4 e = (p + q) + (c + d);
     float t = (e[0] + e[1]) + (e[2] + e[3]);
+    if (NRM && GEMV_NRM_LATE) t = t * rn;
     if (abias) t += (float)b;
     return (float)(_Float16)t;  // F.linear's fp16 output
   };
+  float sqv = 0.f;  // sq_out: this thread's output squared
   if (oval) {  // wave 0 only (tid < NO <= 64)
     if constexpr (EP == kEpSiluMul) {  // 8 outputs per tile and row
       const float g = total(om * kTileN + on, ob0), u = total(om * kTileN + on + 8, ob1);
@@ -558,7 +650,12 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
       float t = total(om * kTileN + on, ob0);
       if constexpr (EP == kEpResidual) t += (float)ores;
       ay[(int64_t)om * a.N + orow] = (_Float16)t;
+      const float f = (float)(_Float16)t;
+      sqv = f * f;
     }
+  }
+  if constexpr (EP == kEpResidual && MT == 1) {
+    if (a.sq_out && wave == 0) sq_tile_out(sqv, a.sq_out, nt);
   }
 }
 
@@ -632,7 +729,8 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
 #define QLIN_GV(PF, T)                                                                     \
   hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, ZM, PF, T>), dim3(blocks), dim3(64 * W), \
                      0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias,             \
-                     (_Float16*)y, M, N, K, group, gs, tpw, (const _Float16*)e.res, e.ep, e.aq)
+                     (_Float16*)y, M, N, K, group, gs, tpw, (const _Float16*)e.res, e.ep, e.aq,   \
+                     e.sq_out)
   if constexpr (MT >= 8) {  // x registers of 4 tiles in flight would spill
     if (ntb == 2) QLIN_GV(2, 2);
     else QLIN_GV(2, 1);
@@ -692,11 +790,20 @@ bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
 template <int BITS, int MT, int ZM>
 int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                 uint16_t* y, int M, int N, int K, int group, int W, int lw, int tpw,
-                hipStream_t st, const Ep& e, const float* nw = nullptr, float eps = 0.f) {
+                hipStream_t st, const Ep& e, const float* nw = nullptr, float eps = 0.f,
+                const NormIn* ni = nullptr) {
   const int Nt = (N + kTileN - 1) / kTileN;
   FastArgs a;
   a.nw = nw;
   a.eps = eps;
+  a.sq_out = e.sq_out;
+  a.sq_in = ni ? ni->sq_in : nullptr;
+  a.sq_n = ni ? ni->sq_n : 0;
+  a.rope_pos = ni ? ni->rope_pos : nullptr;
+  a.rope_cos = ni ? ni->rope_cos : nullptr;
+  a.rope_sin = ni ? ni->rope_sin : nullptr;
+  a.rope_rows = ni ? ni->rope_rows : 0;
+  a.rope_out = ni ? ni->rope_out : nullptr;
   a.qw = qw;
   a.qsz = qsz;
   a.x = (const _Float16*)x;
@@ -785,9 +892,10 @@ extern "C" int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, in
 int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                   const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M,
                   int64_t N, int64_t K, int bits, int group, int epilogue, int act_bits,
-                  int act_flags, void* stream) {
+                  int act_flags, void* stream, float* sq_out) {
   if (!qweight || !qsz || !x || !y || M < 1 || M > kGemvMaxM || !valid_layout(N, K, bits, group))
     return QLIN_EINVAL;
+  if (sq_out && (M != 1 || epilogue != kEpResidual)) return QLIN_EINVAL;
   if (act_bits && (act_bits < 2 || act_bits > 8 || K % 8 || ((uintptr_t)x & 15))) return QLIN_EINVAL;
   if (N == 0) return QLIN_OK;
   ActQ aq{act_bits != 0, act_bits, act_flags, 0.f, 0.f};
@@ -796,7 +904,7 @@ int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const
     aq.qmin = has_zp ? 0.f : -(float)(1 << (act_bits - 1));
     aq.qmax = has_zp ? (float)((1 << act_bits) - 1) : (float)((1 << (act_bits - 1)) - 1);
   }
-  const Ep e{residual, epilogue, aq};
+  const Ep e{residual, epilogue, aq, sq_out};
   hipStream_t st = (hipStream_t)stream;
   const int m = (int)M, n = (int)N, k = (int)K;
   const int zm = zero_mode(flags);
@@ -834,13 +942,24 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
                                           const uint16_t* x, const float* norm_weight, float eps,
                                           const uint16_t* bias, const uint16_t* residual,
                                           uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
-                                          int group, int epilogue, void* stream) {
+                                          int group, int epilogue, const float* sumsq_in,
+                                          int64_t sumsq_n, const int64_t* rope_pos,
+                                          const float* rope_cos, const float* rope_sin,
+                                          int64_t rope_rows, float* rope_out, void* stream) {
   if (!qweight || !qsz || !x || !norm_weight || !y || !rmsnorm_linear_ok(M, N, K, bits, group) ||
       ((uintptr_t)norm_weight & 7) || ((uintptr_t)x & 3) || !(eps >= 0.f) ||
       epilogue < kEpNone || epilogue > kEpSiluMul || (epilogue == kEpResidual && !residual) ||
       (epilogue == kEpSiluMul && N % kTileN))
     return QLIN_EINVAL;
+  // precomputed statistics: one partial per 16 elements of x (the producing launch's tiles)
+  if (sumsq_in && (sumsq_n != (K + kTileN - 1) / kTileN || sumsq_n > 64 * kSqMaxPerLane))
+    return QLIN_EINVAL;
+  if (rope_out && (!rope_pos || !rope_cos || !rope_sin || rope_rows < 1 ||
+                   ((uintptr_t)rope_out & 15) || ((uintptr_t)rope_cos & 15) ||
+                   ((uintptr_t)rope_sin & 15)))
+    return QLIN_EINVAL;
   const Ep e{residual, epilogue, ActQ{false, 0, 0, 0.f, 0.f}};
+  const NormIn ni{sumsq_in, (int)sumsq_n, rope_pos, rope_cos, rope_sin, rope_rows, rope_out};
   hipStream_t st = (hipStream_t)stream;
   const int n = (int)N, k = (int)K;
   int W = 0, lw = 0, tpw = 0;
@@ -849,12 +968,12 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
 #define QLIN_N(B)                                                                             \
   return zm == kZFloat                                                                        \
              ? launch_fast<B, 1, kZFloat>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw, tpw, \
-                                          st, e, norm_weight, eps)                            \
+                                          st, e, norm_weight, eps, &ni)                       \
          : zm == kZWide                                                                       \
              ? launch_fast<B, 1, kZWide>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw, tpw,  \
-                                         st, e, norm_weight, eps)                             \
+                                         st, e, norm_weight, eps, &ni)                        \
              : launch_fast<B, 1, kZNarrow>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw,     \
-                                           tpw, st, e, norm_weight, eps)
+                                           tpw, st, e, norm_weight, eps, &ni)
   switch (bits) {
     case 2: QLIN_N(2);
     case 3: QLIN_N(3);
@@ -862,6 +981,16 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
     default: QLIN_N(8);
   }
 #undef QLIN_N
+}
+
+extern "C" int qlin_linear_res_sumsq_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
+                                         const uint16_t* x, const uint16_t* bias,
+                                         const uint16_t* residual, uint16_t* y, int64_t N,
+                                         int64_t K, int bits, int group, float* sumsq_out,
+                                         void* stream) {
+  if (!residual || !sumsq_out) return QLIN_EINVAL;
+  return qlin::gemv_ep(qweight, qsz, flags, x, bias, residual, y, 1, N, K, bits, group,
+                       kEpResidual, 0, 0, stream, sumsq_out);
 }
 
 extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,

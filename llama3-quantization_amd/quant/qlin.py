@@ -16,7 +16,7 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -58,7 +58,8 @@ SIGNATURES = {
                                _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p], _i),
     "qlin_rmsnorm_linear_supported": ([_l, _l, _l, _i, _i], _i),
     "qlin_rmsnorm_linear_ep_f16": ([_p, _p, _i, _p, _p, ctypes.c_float, _p, _p, _p, _l, _l, _l,
-                                    _i, _i, _i, _p], _i),
+                                    _i, _i, _i, _p, _l, _p, _p, _p, _l, _p, _p], _i),
+    "qlin_linear_res_sumsq_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _i, _i, _p, _p], _i),
     "qlin_rope_kv_f16": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _p, _l, _l, _l, _l,
                           _i, _i, _i, _p], _i),
     "qlin_attn_scores_f32": ([_p, _p, _i, _l, _l, _l, _l, _l, ctypes.c_float, _p], _i),
@@ -417,11 +418,14 @@ def rmsnorm_linear_supported(M, N, K, bits, group):
 
 
 def rmsnorm_linear_ep(x, norm_weight, eps, qweight, qsz, bias, N, K, bits, group, flags=0,
-                      epilogue=EP_NONE, residual=None):
+                      epilogue=EP_NONE, residual=None, sumsq=None, rope=None):
     """``qlin_rmsnorm_linear_ep_f16``: ``linear_ep(rmsnorm(x))`` for one token row in ONE launch —
     x fp16 [.., K] is the hidden state BEFORE the RMSNorm (norm_weight fp32 [K], eps), which the
     GEMV applies to its x words itself (the sum of squares in another order than ``rmsnorm``:
-    the normed x can differ from it by an fp16 ulp)."""
+    the normed x can differ from it by an fp16 ulp).  ``sumsq``: fp32 [ceil(K/16)] partial sums of
+    squares of x written by ``linear_res_sumsq`` (precomputed statistics); ``rope``: (position_ids,
+    cos fp32 [rows, 128], sin, out fp32 [256]) — the launch also copies that position's cos / sin
+    rows into ``out`` for ``attn_decode_rope(..., position_ids=None)``."""
     _dev(x, qweight, qsz, bias, residual, norm_weight)
     if x.dtype != torch.float16 or norm_weight.dtype != torch.float32:
         raise ValueError("rmsnorm_linear_ep takes fp16 x and an fp32 norm weight")
@@ -438,10 +442,49 @@ def rmsnorm_linear_ep(x, norm_weight, eps, qweight, qsz, bias, N, K, bits, group
     if epilogue == EP_RESIDUAL:
         if residual is None or residual.dtype != torch.float16 or residual.shape != y.shape:
             raise ValueError(f"residual must be fp16 {tuple(y.shape)}")
+    sq_n = 0
+    if sumsq is not None:
+        _on_gpu(sumsq)
+        if sumsq.dtype != torch.float32 or sumsq.numel() != (K + 15) // 16 or \
+                not sumsq.is_contiguous():
+            raise ValueError(f"sumsq must be fp32 [{(K + 15) // 16}]")
+        sq_n = sumsq.numel()
+    rp = rc_ = rs_ = ro = None
+    rows = 0
+    if rope is not None:
+        rp, rc_, rs_, ro = rope
+        _on_gpu(rp, rc_, rs_, ro)
+        if ro.dtype != torch.float32 or ro.numel() < 256 or rc_.dtype != torch.float32 or \
+                rs_.dtype != torch.float32 or not (rc_.is_contiguous() and rs_.is_contiguous()):
+            raise ValueError("rope: fp32 cos / sin caches and an fp32 [256] output")
+        rp = rp.reshape(-1)[:1].to(torch.int64).contiguous()
+        rows = rc_.shape[0]
     rc = load_library().qlin_rmsnorm_linear_ep_f16(
         _ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(norm_weight), float(eps), _ptr(bias),
-        _ptr(residual), _ptr(y), M, N, K, bits, group, epilogue, _stream(x))
+        _ptr(residual), _ptr(y), M, N, K, bits, group, epilogue, _ptr(sumsq), sq_n, _ptr(rp),
+        _ptr(rc_), _ptr(rs_), rows, _ptr(ro), _stream(x))
     _check(rc, "qlin_rmsnorm_linear_ep_f16")
+    return y
+
+
+def linear_res_sumsq(x, qweight, qsz, bias, N, K, bits, group, flags, residual, sumsq_out):
+    """``qlin_linear_res_sumsq_f16``: one token row ``residual + F.linear(x)`` that also writes
+    ``sumsq_out`` (fp32 [ceil(N/16)]: per 16 outputs, the sum of their squares) — the statistics
+    of the RMSNorm that reads the output next (``rmsnorm_linear_ep(..., sumsq=...)``)."""
+    _dev(x, qweight, qsz, bias, residual, sumsq_out)
+    if x.dtype != torch.float16 or x.shape[-1] != K or x.numel() != K:
+        raise ValueError(f"linear_res_sumsq takes one fp16 row of {K} features")
+    _check_packed(qweight, qsz, N, K, bits, group)
+    y = torch.empty(*x.shape[:-1], N, dtype=torch.float16, device=x.device)
+    if residual is None or residual.dtype != torch.float16 or residual.shape != y.shape:
+        raise ValueError(f"residual must be fp16 {tuple(y.shape)}")
+    if sumsq_out.dtype != torch.float32 or sumsq_out.numel() != (N + 15) // 16:
+        raise ValueError(f"sumsq_out must be fp32 [{(N + 15) // 16}]")
+    b = None if bias is None else bias.to(torch.float16).contiguous()
+    rc = load_library().qlin_linear_res_sumsq_f16(
+        _ptr(qweight), _ptr(qsz), flags, _ptr(x.contiguous()), _ptr(b), _ptr(residual.contiguous()),
+        _ptr(y), N, K, bits, group, _ptr(sumsq_out), _stream(x))
+    _check(rc, "qlin_linear_res_sumsq_f16")
     return y
 
 
@@ -693,7 +736,13 @@ def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_
     if cos_cache.dtype != torch.float32 or not cos_cache.is_contiguous() or \
             sin_cache.dtype != torch.float32 or not sin_cache.is_contiguous():
         raise ValueError("rope takes contiguous fp32 cos / sin caches")
-    pos, pbs = _pos_ids(position_ids, B, 1)
+    if position_ids is None:
+        # cos_cache / sin_cache are the step's own rows (rmsnorm_linear_ep(..., rope=...))
+        if B != 1:
+            raise ValueError("attn_decode_rope: position_ids None needs batch 1")
+        pos, pbs = None, 0
+    else:
+        pos, pbs = _pos_ids(position_ids, B, 1)
     m = None
     if mask is not None:
         if mask.dtype != torch.float16 or mask.shape[-1] != L or mask.shape[-2] != 1:

@@ -61,6 +61,13 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert ep(p, p, 0, p, None, None, p, 1, 16, 64, 4, 64, 0, 9, 0, None, 0, None) == 1  # act bits
     assert ep(p, p, 0, p, None, None, p, 100, 16, 64, 4, 64, 0, 8, 0, None, 0, None) == 1  # no ws
     assert ep(p, p, 0, p, None, None, p, 100, 16, 64, 4, 64, 0, 8, 0, p, 64, None) == 1  # short ws
+    # ABI 8: residual + statistics needs its partials buffer; precomputed statistics must be
+    # one partial per 16 features of x
+    assert lib.qlin_linear_res_sumsq_f16(p, p, 0, p, None, p, p, 16, 64, 4, 64, None, None) == 1
+    assert lib.qlin_rmsnorm_linear_ep_f16(p, p, 0, p, p, 1e-5, None, None, p, 1, 16, 128, 4, 128,
+                                          0, p, 3, None, None, None, 0, None, None) == 1
+    assert lib.qlin_rmsnorm_linear_ep_f16(p, p, 0, p, p, 1e-5, None, None, p, 1, 16, 128, 4, 128,
+                                          0, None, 0, None, None, None, 0, p, None) == 1  # rope
     assert lib.qlin_pack_codes(None, 16, 64, 4, None, None) == 1
     assert lib.qlin_pack_codes(p, 16, 48, 4, p, None) == 1  # K % 32
     assert lib.qlin_pack_codes(p, 16, 64, 5, p, None) == 1  # bits
