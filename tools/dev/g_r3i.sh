@@ -8,3 +8,9 @@ for r in 1 2; do
   run QLIN_DEV_NO_ROPE_GATHER=1
   run QLIN_DEV_NO_SUMSQ=1 QLIN_DEV_NO_ROPE_GATHER=1
 done
+for r in 1 2; do
+  run QLIN_LIBRARY=tools/dev/libnrm_late.so
+  run QLIN_LIBRARY=tools/dev/libnrm_late.so QLIN_DEV_NO_SUMSQ=1
+done
+QLIN_LIBRARY=tools/dev/libnrm_late.so timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_epilogue.py -p no:cacheprovider -k rmsnorm > $O/t_late.log 2>&1; echo late-tests rc=$?; tail -3 $O/t_late.log
+QLIN_LIBRARY=tools/dev/libnrm_late.so QLIN_PARITY_OUT=$O/r3_decode_parity_late.json timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_decode.py -p no:cacheprovider -k decode_three_way > $O/t_dl.log 2>&1; echo rc=$?; tail -2 $O/t_dl.log
