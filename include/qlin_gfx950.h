@@ -223,11 +223,14 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
  * RMSNorm + packed linear for ONE token row in one launch (the decoder layer's
  * input_layernorm -> fused q/k/v and post_attention_layernorm -> gate/up at decode; the norm is
  * OmniLlamaRMSNorm, quant/omni_norm.py:52-63 of the reference): x fp16 [K] is the hidden state
- * BEFORE the norm, norm_weight fp32 [K] (8-B aligned), eps its variance epsilon; the GEMV blocks
- * compute mean(x^2) themselves and normalise their x words (weight * (x * rsqrt(mean + eps)),
- * rounded to fp16) before the dequant-MFMA, then apply `epilogue` as qlin_linear_ep_f16 does.
- * The sum of squares runs in another order than qlin_rmsnorm_f16's, so a normed value can differ
- * from that kernel's by an fp16 ulp.  Supported: M == 1 on the fast GEMV path (K % 128 == 0,
+ * BEFORE the norm, norm_weight fp32 [K] (8-B aligned), eps its variance epsilon.  The GEMV
+ * multiplies RN16(weight * x) (fp32 product, one fp16 rounding) and applies r = rsqrt(mean(x^2) +
+ * eps) to the fp32 accumulators before F.linear's fp16 rounding: y = RN16(r * sum W_dq (w x)), then
+ * `epilogue` as qlin_linear_ep_f16 — the norm's statistics (summed by the blocks from the x words
+ * they load anyway) are needed only at the end, so the first MFMAs wait for nothing (round 3; the
+ * round-2 form normalised x first, behind a barrier: 2 us more per decode layer).  The same
+ * mathematics as the reference's RN16(w * (x * r)) with the fp16 rounding at another point:
+ * outputs within a few fp16 ulps of the two launches (qlin_rmsnorm_f16, then the linear).  Supported: M == 1 on the fast GEMV path (K % 128 == 0,
  * group % 128 == 0 or group in {32, 64}, <= 4 weight tiles per wave) —
  * qlin_rmsnorm_linear_supported() says so (1) or not (0); otherwise QLIN_EINVAL.
  */
@@ -236,13 +239,16 @@ int qlin_rmsnorm_linear_supported(int64_t M, int64_t N, int64_t K, int bits, int
  * qlin_rmsnorm_linear_ep_f16 optional inputs (ABI 8), for the decode chain of a fused layer:
  *   sumsq_in / sumsq_n  precomputed statistics: sumsq_n == ceil(K / 16) partial sums of squares
  *                       of x, one per 16 consecutive elements, as qlin_linear_res_sumsq_f16 writes
- *                       them while producing x; the norm then uses sum(partials) / K (a fixed
- *                       order, the same in every block) instead of reducing x in every block
- *                       behind a barrier.  NULL: computed in the kernel.  K <= 8192.
+ *                       them while producing x; r then comes from sum(partials) / K (a fixed
+ *                       order) instead of the blocks' own sums.  NULL: computed in the kernel.
+ *                       K <= 8192.  (Measured on the LLaMA3-8B decode layer: no gain over the
+ *                       in-kernel sums since the late rsqrt; the fused layer does not use it.)
  *   rope_pos / rope_cos / rope_sin / rope_rows / rope_out  copy the RoPE cos and sin rows of
  *                       position rope_pos[0] (clamped to [0, rope_rows)) of the fp32 caches
  *                       [rope_rows][128] into rope_out[0..127] / [128..255] (16-B aligned), for a
  *                       following qlin_attn_decode_rope with position_ids NULL.  NULL: skipped.
+ *                       (Measured: the attention launch is not shortened by it; unused by the
+ *                       fused layer.)
  */
 int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                                const uint16_t* x, const float* norm_weight, float eps,

@@ -370,12 +370,9 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
 #ifndef GEMV_NRM_XFIRST  // dev switch: the fused norm's x words issued before the codes
 #define GEMV_NRM_XFIRST 1
 #endif
-#ifndef GEMV_NRM_LATE  // 1: the norm's rsqrt applied to the accumulators in the epilogue (x words
-#define GEMV_NRM_LATE 0  // rounded as RN16(w * x)): the first MFMAs wait for no statistics
-#endif
-#ifndef GEMV_NRM_ABLATE  // dev ablation (wrong results): 1 = no in-kernel statistics (constant
-#define GEMV_NRM_ABLATE 0  // rsqrt, no barrier): the upper bound of precomputed statistics
-#endif
+#ifndef GEMV_NRM_LATE  // 1 (round 3): the norm's rsqrt is applied to the accumulators in the
+#define GEMV_NRM_LATE 1  // epilogue (x words rounded as RN16(w * x)): the first MFMAs wait for no
+#endif                   // statistics; 0: the round-2 form (statistics behind a barrier first)
 // qlin_rmsnorm_linear_ep_f16's optional inputs (precomputed statistics, RoPE row gather)
 struct NormIn {
   const float* sq_in;
@@ -443,7 +440,7 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   // precomputed norm statistics: issued before every other load (in-order completion: the norm
   // then waits for these alone, not for the weights)
   float sqp[NRM ? kSqMaxPerLane : 1];
-  if constexpr (NRM) {
+  if constexpr (NRM && !GEMV_NRM_LATE) {
     if (a.sq_in) {
 #pragma unroll
       for (int i = 0; i < kSqMaxPerLane; ++i) sqp[i] = a.sq_in[min(lane + 64 * i, a.sq_n - 1)];
@@ -536,8 +533,6 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
         ss_late = ss_late + f1 * f1;
       }
     }
-  } else if constexpr (NRM && GEMV_NRM_ABLATE) {
-    rn = rsqrtf(1.f + a.eps);
   } else if constexpr (NRM) {
    if (a.sq_in) {
 #pragma clang fp contract(off)
@@ -628,9 +623,16 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   }
   __syncthreads();
   if constexpr (NRM && GEMV_NRM_LATE) {
-    float tot = 0.f;
-    for (int w = 0; w < a.W; ++w) tot += nss[w];
-    rn = rsqrtf(tot / (float)a.K + a.eps);
+    if (wave == 0) {  // the outputs are formed by wave 0
+#pragma clang fp contract(off)
+      float tot = 0.f;
+      if (a.sq_in) {  // precomputed statistics (fixed order: every block forms the same value)
+        for (int i = 0; i < a.sq_n; ++i) tot += a.sq_in[i];
+      } else {
+        for (int w = 0; w < a.W; ++w) tot += nss[w];
+      }
+      rn = rsqrtf(tot / (float)a.K + a.eps);
+    }
   }
   auto total = [&](int o, _Float16 b) {
     const f4* r = reinterpret_cast<const f4*>(red + o * kMaxWaves);

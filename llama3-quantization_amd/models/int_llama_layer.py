@@ -13,7 +13,6 @@ attention matmuls (fp32 attention core, as the reference intends), and the atten
 cast back to the layer's activation dtype before o_proj.  In fp32 this is exactly the reference.
 """
 import math
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -88,9 +87,6 @@ def _act(name):
     if name in ("gelu", "gelu_new", "gelu_pytorch_tanh"):
         return (lambda x: nn.functional.gelu(x, approximate="tanh")) if name != "gelu" else nn.functional.gelu
     raise ValueError(f"unsupported hidden_act {name}")
-
-
-_DEV_NO_ROPE_GATHER = bool(os.environ.get("QLIN_DEV_NO_ROPE_GATHER"))  # dev A/B switch
 
 
 class QuantLlamaMLP(nn.Module):
@@ -258,23 +254,21 @@ class QuantLlamaAttention(nn.Module):
                 return False
         return True
 
-    def _project(self, hidden_states, prenorm=None, rope=None):
-        """(q, k, v, rope_done) of the (normed) hidden state; ``prenorm``: hidden_states is the
-        input of that RMSNorm module, applied here — for one token row inside the fused q/k/v
-        launch, which then also gathers the ``rope`` row (rope_done True)."""
+    def _project(self, hidden_states, prenorm=None):
+        """q, k, v of the (normed) hidden state; ``prenorm``: hidden_states is the input of that
+        RMSNorm module, applied here — for one token row inside the fused q/k/v launch."""
         if self.qkv is not None:
             act = _same_act([self.q_proj, self.k_proj, self.v_proj])
             if act is not None:
                 norm = prenorm.fusable(hidden_states) if prenorm is not None else None
                 if norm is not None and self.qkv.prenorm_ok(hidden_states, act):
-                    return (*self.qkv.forward_prenorm(hidden_states, norm, rope), rope is not None)
+                    return self.qkv.forward_prenorm(hidden_states, norm)
                 if prenorm is not None:
                     hidden_states = prenorm(hidden_states)
-                return (*self.qkv(hidden_states, act), False)
+                return self.qkv(hidden_states, act)
         if prenorm is not None:
             hidden_states = prenorm(hidden_states)
-        return (self.q_proj(hidden_states), self.k_proj(hidden_states),
-                self.v_proj(hidden_states), False)
+        return self.q_proj(hidden_states), self.k_proj(hidden_states), self.v_proj(hidden_states)
 
     def _decode_kernel_ok(self, hidden_states, attention_mask, past_key_value, use_cache,
                           output_attentions, kv_seq_len):
@@ -337,13 +331,7 @@ class QuantLlamaAttention(nn.Module):
             position_ids = torch.arange(kv_seq_len - q_len, kv_seq_len, device=hidden_states.device)[None]
         decode = self._decode_kernel_ok(hidden_states, attention_mask, past_key_value, use_cache,
                                         output_attentions, kv_seq_len)
-        rope = None
-        if decode and bsz == 1 and not _DEV_NO_ROPE_GATHER:
-            # the q/k/v launch gathers this position's cos / sin rows for the attention launch
-            cos_c, sin_c = self._rope_cache(hidden_states, kv_seq_len)
-            rope = (position_ids, cos_c, sin_c,
-                    torch.empty(2, self.head_dim, dtype=torch.float32, device=hidden_states.device))
-        q, k, v, rope_done = self._project(hidden_states, prenorm, rope)
+        q, k, v = self._project(hidden_states, prenorm)
         value_states = v.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
         appended = False
         if self.rope_kernel and q.dtype == torch.float16 and q.is_cuda:
@@ -354,11 +342,8 @@ class QuantLlamaAttention(nn.Module):
             if decode:
                 # one launch: RoPE, the cache append and the decode attention
                 buf, L0 = self._cache_for(past_key_value, bsz, 1, q.device)
-                rc_, rs_, rpos = cos_c, sin_c, position_ids
-                if rope_done:  # the step's rows, gathered by the q/k/v launch
-                    rc_, rs_, rpos = rope[3][0:1], rope[3][1:2], None
                 attn_output = qlin.attn_decode_rope(
-                    q, k, v, rc_, rs_, rpos, self.num_heads, self.num_key_value_heads,
+                    q, k, v, cos_c, sin_c, position_ids, self.num_heads, self.num_key_value_heads,
                     self.head_dim, buf[0], buf[1], L0, attention_mask, math.sqrt(self.head_dim),
                     out_dtype=act_dtype if act_dtype == torch.float16 else torch.float32)
                 past_key_value = (buf[0][:, :, :L0 + 1], buf[1][:, :, :L0 + 1]) if use_cache else None

@@ -243,13 +243,11 @@ class FusedPackedLinear(nn.Module):
                 and qlin.rmsnorm_linear_supported(1, self.out_features, self.in_features,
                                                   self.wbits, self.group))
 
-    def forward_prenorm(self, x, norm, rope=None):
-        """``forward(rmsnorm(x))`` in one launch; ``norm`` = (fp32 weight, eps); the norm's
-        statistics come precomputed when x carries them (``sumsq_of``); ``rope``: see
-        ``qlin.rmsnorm_linear_ep``."""
+    def forward_prenorm(self, x, norm):
+        """``forward(rmsnorm(x))`` in one launch; ``norm`` = (fp32 weight, eps)."""
         y = qlin.rmsnorm_linear_ep(x.contiguous(), norm[0], norm[1], self.qweight, self.qsz,
                                    self.bias, self.out_features, self.in_features, self.wbits,
-                                   self.group, self.qflags, sumsq=sumsq_of(x), rope=rope)
+                                   self.group, self.qflags)
         return torch.split(y, self.splits, dim=-1)
 
     def forward(self, x, act=(0, 0)):
@@ -303,12 +301,11 @@ class SiluMulPackedLinear(nn.Module):
                                                   self.wbits, self.group))
 
     def forward_prenorm(self, x, norm):
-        """``forward(rmsnorm(x))`` in one launch; ``norm`` = (fp32 weight, eps); the norm's
-        statistics come precomputed when x carries them (``sumsq_of``)."""
+        """``forward(rmsnorm(x))`` in one launch; ``norm`` = (fp32 weight, eps)."""
         return qlin.rmsnorm_linear_ep(x.contiguous(), norm[0], norm[1], self.qweight, self.qsz,
                                       self.bias, 2 * self.out_features, self.in_features,
                                       self.wbits, self.group, self.qflags,
-                                      epilogue=qlin.EP_SILU_MUL, sumsq=sumsq_of(x))
+                                      epilogue=qlin.EP_SILU_MUL)
 
     def forward(self, x, act=(0, 0)):
         xin = x if x.dtype == torch.float16 else x.to(torch.float16)
@@ -319,38 +316,14 @@ class SiluMulPackedLinear(nn.Module):
         return y if x.dtype == torch.float16 else y.to(x.dtype)
 
 
-_DEV_NO_SUMSQ = bool(os.environ.get("QLIN_DEV_NO_SUMSQ"))  # dev A/B switch
-
-
-def sumsq_of(x):
-    """The RMSNorm statistics ``packed_residual_linear`` attached to the tensor it returned (fp32
-    partial sums of squares, one per 16 features), if x is that very tensor, unmodified since;
-    else None (the norm then reduces x itself)."""
-    ent = getattr(x, "_qlin_sumsq", None)
-    if ent is None or ent[1] != x._version:
-        return None
-    return ent[0]
-
-
 def packed_residual_linear(lin, x, residual):
     """``residual + lin(x)`` for a packed QuantLinear as one launch (``QLIN_EP_RESIDUAL``): the
-    decoder layer's residual add fused into o_proj / down_proj's output.  For one fp16 token row
-    the launch also writes the sums of squares of its output (``qlin.linear_res_sumsq``), attached
-    to the returned tensor for the RMSNorm that reads it next (``sumsq_of``)."""
+    decoder layer's residual add fused into o_proj / down_proj's output."""
     xin = x if x.dtype == torch.float16 else x.to(torch.float16)
     bias = None if lin.bias is None else lin.bias.to(torch.float16).contiguous()
     act = act_spec(lin)
     if act is None:
         raise ValueError("the act quantizer of this linear cannot be fused")
-    if (not _DEV_NO_SUMSQ and act == (0, 0) and xin.numel() == lin.in_features
-            and residual.dtype == torch.float16
-            and residual.numel() == lin.out_features and xin.is_cuda):
-        sq = torch.empty((lin.out_features + 15) // 16, dtype=torch.float32, device=xin.device)
-        y = qlin.linear_res_sumsq(xin.reshape(residual.shape[:-1] + (lin.in_features,)),
-                                  lin.qweight, lin.qsz, bias, lin.out_features, lin.in_features,
-                                  lin.wbits, lin.group, lin.qflags, residual.contiguous(), sq)
-        y._qlin_sumsq = (sq, y._version)
-        return y
     return qlin.linear_ep(xin.contiguous(), lin.qweight, lin.qsz, bias, lin.out_features,
                           lin.in_features, lin.wbits, lin.group, lin.qflags,
                           epilogue=qlin.EP_RESIDUAL, residual=residual.contiguous(),
