@@ -28,13 +28,19 @@ find "$OUT/kt" -name "*kernel_stats.csv" -exec cp {} "$OUT/${R}_gemv_int4_g128_k
 # FETCH_SIZE per dispatch, one pass per mode: the batched streaming launch (headline) and the
 # dependent single launches (other_mode)
 (cd /tmp && step pmc 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run \
-   -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode) || exit $?
+   -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode --no-decode-layer) || exit $?
 python tools/pmc_traffic.py "$OUT/pmc" gemv_stream gemv_int4_g128_batched \
   "$OUT/${R}_gemv_int4_g128_batched_pmc.json"
 (cd /tmp && step pmc_launches 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcl" \
    -o run -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode \
-   --mode launches) || exit $?
-python tools/pmc_traffic.py "$OUT/pmcl" gemv_fast gemv_int4_g128 "$OUT/${R}_gemv_int4_g128_pmc.json"
+   --no-decode-layer --mode launches) || exit $?
+python tools/pmc_traffic.py "$OUT/pmcl" "gemv_fast_kernel<4, 1, 1, 0, 0, 2, false>" gemv_int4_g128 \
+  "$OUT/${R}_gemv_int4_g128_pmc.json"
+# the decode layer's traffic: every GEMV / attention dispatch of a --no-other-mode run
+(cd /tmp && step pmc_decode 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcd" -o run \
+   -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode --ramp-s 0) \
+   || exit $?
+python tools/decode_traffic.py "$OUT/pmcd" "$OUT/${R}_decode_layer_int4_g128_pmc.json"
 step decode_layer 300 python tools/bench_decode.py
 step attn_prefill 300 python tools/dev/attn_prefill_bench.py
 step ppl_llama3_8b 500 python tools/ppl_llama3_8b.py
