@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 8
+#define QLIN_ABI_VERSION 9
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -286,7 +286,9 @@ int qlin_linear_res_sumsq_f16(const uint32_t* qweight, const uint32_t* qsz, int 
  * of `partials` scratch a call needs (0: none, pass NULL; -1: unsupported shapes); `counters` is
  * int32 [>= B * Hkv], zero-filled before its first use and left zero-filled by every call (the
  * merging block resets it), so one counter buffer serves all later calls on the same stream,
- * graph replays included; do not share it between streams running concurrently.
+ * graph replays included; do not share it between streams running concurrently.  counters NULL
+ * with partials (B == 1, qlin_attn_decode_splits() >= 2): the launch writes the split partials
+ * only and `out` is left untouched — qlin_attn_merge_linear_f16 merges them inside o_proj.
  */
 int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L);
 int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
@@ -312,6 +314,27 @@ int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_
                           uint16_t* v_cache, int64_t kv_head_stride, const uint16_t* mask,
                           void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int D,
                           float scale_div, float* partials, int32_t* counters, void* stream);
+
+/*
+ * The split-L partials of a decode attention launch (qlin_attn_decode / _rope with counters NULL,
+ * B == 1) merged inside o_proj: y = residual + F.linear(attn, W, bias) with attn = the attention
+ * output rounded to fp16 (the layer's .to(fp16)), i.e. qlin_attn_decode(out_dtype QLIN_F16)
+ * followed by qlin_linear_ep_f16(QLIN_EP_RESIDUAL) in one launch — same arithmetic up to the fp32
+ * summation order of the merge.  Replaces the reference's o_proj(attn_output) and the residual
+ * add after it (models/int_llama_layer.py:174, :249) for one decode token.
+ *   partials  as written by the attention launch for (B = 1, Hq, Hkv, L);  qweight / qsz / flags /
+ *   bias / bits / group  the packed o_proj [N, Hq * 128] (narrow or float zeros);  residual, y
+ *   fp16 [N].  qlin_attn_decode_splits(): the split count S of a (B, Hkv, L) launch (1: no
+ *   partials, -1: unsupported); qlin_attn_merge_linear_supported(): 1 when this entry takes the
+ *   shape (2 <= S <= 10, Hq <= 64 heads).
+ */
+int qlin_attn_decode_splits(int64_t B, int Hkv, int64_t L);
+int qlin_attn_merge_linear_supported(int64_t L, int Hq, int Hkv, int64_t N, int bits, int group,
+                                     int flags);
+int qlin_attn_merge_linear_f16(const float* partials, int64_t L, int Hq, int Hkv,
+                               const uint32_t* qweight, const uint32_t* qsz, int flags,
+                               const uint16_t* bias, const uint16_t* residual, uint16_t* y,
+                               int64_t N, int bits, int group, void* stream);
 
 /*
  * Fused prefill attention (many query tokens per sequence): the same attention core as

@@ -20,7 +20,8 @@ from torch import nn
 
 from quant import qlin
 from quant.int_linear import (FusedPackedLinear, QuantLinear, SiluMulPackedLinear, _same_act,
-                              act_spec, packed_residual_linear)
+                              act_spec, attn_merge_ok, packed_attn_merge_linear,
+                              packed_residual_linear)
 from quant.int_matmul import QuantMatMul
 from quant.omni_norm import KERNEL_MAX_ROWS, OmniLlamaRMSNorm
 
@@ -342,11 +343,20 @@ class QuantLlamaAttention(nn.Module):
             if decode:
                 # one launch: RoPE, the cache append and the decode attention
                 buf, L0 = self._cache_for(past_key_value, bsz, 1, q.device)
+                merge = bsz == 1 and attn_merge_ok(self.o_proj, L0 + 1, self.num_heads,
+                                                   self.num_key_value_heads, residual, act_dtype)
                 attn_output = qlin.attn_decode_rope(
                     q, k, v, cos_c, sin_c, position_ids, self.num_heads, self.num_key_value_heads,
                     self.head_dim, buf[0], buf[1], L0, attention_mask, math.sqrt(self.head_dim),
-                    out_dtype=act_dtype if act_dtype == torch.float16 else torch.float32)
+                    out_dtype=act_dtype if act_dtype == torch.float16 else torch.float32,
+                    partials_only=merge)
                 past_key_value = (buf[0][:, :, :L0 + 1], buf[1][:, :, :L0 + 1]) if use_cache else None
+                if merge:
+                    # the split-L merge runs inside o_proj (+ residual): one launch fewer round
+                    # trips than attention-merge-then-o_proj, same arithmetic up to fp32 order
+                    return packed_attn_merge_linear(self.o_proj, attn_output, L0 + 1, self.num_heads,
+                                                    self.num_key_value_heads, residual), \
+                        None, past_key_value
                 attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
                 return self._out(attn_output, residual), None, past_key_value
             if kv_mode:
@@ -373,10 +383,17 @@ class QuantLlamaAttention(nn.Module):
                 and qlin.attn_decode_supported(query_states, key_states, attention_mask)):
             # fused decode attention: same fp32 arithmetic as the path below (repeat_kv, QK^T,
             # / sqrt(d), + mask, clamp, softmax, PV) up to summation order
+            L = key_states.shape[2]
+            merge = bsz == 1 and attn_merge_ok(self.o_proj, L, self.num_heads,
+                                               self.num_key_value_heads, residual, act_dtype)
             attn_output = qlin.attn_decode(query_states, key_states, value_states, attention_mask,
                                            math.sqrt(self.head_dim),
                                            out_dtype=act_dtype if act_dtype == torch.float16
-                                           else torch.float32)
+                                           else torch.float32, partials_only=merge)
+            if merge:  # as in the decode branch above
+                return packed_attn_merge_linear(self.o_proj, attn_output, L, self.num_heads,
+                                                self.num_key_value_heads, residual), \
+                    None, past_key_value
             attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
             return self._out(attn_output, residual), None, past_key_value
 

@@ -16,7 +16,7 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -69,6 +69,9 @@ SIGNATURES = {
     "qlin_attn_decode": ([_p, _p, _p, _p, _p, _i, _l, _i, _i, _l, _i, _l, ctypes.c_float, _p, _p,
                           _p],
                          _i),
+    "qlin_attn_decode_splits": ([_l, _i, _l], _i),
+    "qlin_attn_merge_linear_supported": ([_l, _i, _i, _l, _i, _i, _i], _i),
+    "qlin_attn_merge_linear_f16": ([_p, _l, _i, _i, _p, _p, _i, _p, _p, _p, _l, _i, _i, _p], _i),
     "qlin_decode_supported": ([_i, _l, _l, _i, _i, _i, _i, _i, _i], _i),
     "qlin_decode_workspace_bytes": ([_i, _l, _l, _i, _i, _i, _l], _l),
     "qlin_decode_llama_f16": ([_p, _i, _l, _l, _i, _i, _i, _i, _i, _i, ctypes.c_float, _p, _p, _p,
@@ -673,11 +676,12 @@ def _cache_head_stride(k, v):
     return hs
 
 
-def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32):
+def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32, partials_only=False):
     """softmax(q k^T / scale_div + mask) v for one query token: q fp32 [B, Hq, 1, D], k/v fp16
     [B, Hkv, L, D], mask fp16 [B, 1, 1, L] or None -> [B, Hq, 1, D] in out_dtype (fp32, or the
     fp32 result rounded to fp16 in the kernel); k / v may be row-prefix views of KV cache
-    buffers (rope_kv), read in place."""
+    buffers (rope_kv), read in place.  partials_only (``attn_merge_linear_supported``): returns
+    the split-L partials for ``attn_merge_linear`` instead (no merge in this launch)."""
     _on_gpu(q, k, v)
     if not attn_decode_supported(q, k, mask):
         raise ValueError("attn_decode: unsupported shapes / dtypes")
@@ -694,28 +698,67 @@ def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32):
             mask.expand(B, 1, 1, L).reshape(B, L).contiguous()
     out = torch.empty(B, Hq, 1, D, dtype=out_dtype, device=q.device)
     lib = load_library()
-    nbytes = lib.qlin_attn_decode_partials_bytes(B, Hq, Hkv, L)
-    if nbytes < 0:
-        raise ValueError("attn_decode: unsupported shapes")
-    part = cnt = None
-    if nbytes:
-        part = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
-        cnt = _attn_counters(q.device, B * Hkv)
+    part, cnt = _attn_partials(lib, q.device, B, Hq, Hkv, L, partials_only)
     rc = lib.qlin_attn_decode(_ptr(q.contiguous()), _ptr(k), _ptr(v), _ptr(m), _ptr(out),
                               _dtcode(out),
                               B, Hq, Hkv, L, D, hs, float(scale_div), _ptr(part), _ptr(cnt),
                               _stream(q))
     _check(rc, "qlin_attn_decode")
-    return out
+    return part if partials_only else out
+
+
+def _attn_partials(lib, device, B, Hq, Hkv, L, partials_only):
+    """(partials scratch, merge counters) of a decode attention launch; partials_only: counters
+    None (the launch stops after writing the partials)."""
+    nbytes = lib.qlin_attn_decode_partials_bytes(B, Hq, Hkv, L)
+    if nbytes < 0:
+        raise ValueError("attn_decode: unsupported shapes")
+    if partials_only and (B != 1 or nbytes == 0):
+        raise ValueError("attn_decode partials_only: batch 1 with a split cache (see "
+                         "attn_merge_linear_supported)")
+    if not nbytes:
+        return None, None
+    part = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+    return part, (None if partials_only else _attn_counters(device, B * Hkv))
+
+
+def attn_merge_linear_supported(L, Hq, Hkv, N, bits, group, flags=0):
+    """Whether ``attn_merge_linear`` takes a decode step over L cache rows (batch 1)."""
+    return bool(load_library().qlin_attn_merge_linear_supported(L, Hq, Hkv, N, bits, group, flags))
+
+
+def attn_merge_linear(partials, L, Hq, Hkv, qweight, qsz, bias, residual, N, bits, group,
+                      flags=0):
+    """``qlin_attn_merge_linear_f16``: ``residual + o_proj(attn)`` for one decode token, attn the
+    split-L partials of ``attn_decode(..., partials_only=True)`` (or ``attn_decode_rope``) merged
+    and rounded to fp16 inside the o_proj launch.  residual fp16 [.., N] (one row) -> y like it."""
+    _dev(partials, qweight, qsz, bias, residual)
+    K = Hq * ATTN_D
+    _check_packed(qweight, qsz, N, K, bits, group)
+    if residual.dtype != torch.float16 or residual.numel() != N:
+        raise ValueError(f"residual must be one fp16 row of {N}")
+    if bias is not None and (bias.dtype != torch.float16 or bias.numel() != N):
+        raise ValueError("bias must be fp16 [N]")
+    lib = load_library()
+    need = lib.qlin_attn_decode_partials_bytes(1, Hq, Hkv, L)
+    if partials.dtype != torch.float32 or partials.numel() * 4 < need or need <= 0:
+        raise ValueError("partials: the fp32 scratch of attn_decode(partials_only=True)")
+    y = torch.empty_like(residual)
+    rc = lib.qlin_attn_merge_linear_f16(_ptr(partials), L, Hq, Hkv, _ptr(qweight), _ptr(qsz),
+                                        flags, _ptr(bias), _ptr(residual), _ptr(y), N, bits,
+                                        group, _stream(residual))
+    _check(rc, "qlin_attn_merge_linear_f16")
+    return y
 
 
 def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim,
-                     k_cache, v_cache, kv0, mask, scale_div, out_dtype=torch.float32):
+                     k_cache, v_cache, kv0, mask, scale_div, out_dtype=torch.float32,
+                     partials_only=False):
     """``qlin_attn_decode_rope``: ``rope_kv`` + ``attn_decode`` in one launch for one new token:
     q [B, 1, Hq*D], k / v [B, 1, Hkv*D] fp16 row-strided views (before RoPE); k_cache / v_cache
     fp16 [B, Hkv, rows, D] contiguous buffers holding rows 0 .. kv0 - 1, row kv0 written here;
     mask fp16 [B, 1, 1, kv0 + 1] or None -> [B, Hq, 1, D] (out_dtype), bit-identical to the two
-    launches."""
+    launches.  partials_only: the split-L partials for ``attn_merge_linear`` instead."""
     for t_ in (q, k, v):
         if _rows(t_) is None:
             raise ValueError("attn_decode_rope takes row-strided [B, 1, H*D] q / k / v")
@@ -751,13 +794,7 @@ def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_
             mask.expand(B, 1, 1, L).reshape(B, L).contiguous()
     out = torch.empty(B, n_heads, 1, head_dim, dtype=out_dtype, device=q.device)
     lib = load_library()
-    nbytes = lib.qlin_attn_decode_partials_bytes(B, n_heads, n_kv_heads, L)
-    if nbytes < 0:
-        raise ValueError("attn_decode_rope: unsupported shapes")
-    part = cnt = None
-    if nbytes:
-        part = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
-        cnt = _attn_counters(q.device, B * n_kv_heads)
+    part, cnt = _attn_partials(lib, q.device, B, n_heads, n_kv_heads, L, partials_only)
     rows = k_cache.shape[2]
     rc = lib.qlin_attn_decode_rope(
         _ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(v), _rows(v), _ptr(cos_cache),
@@ -765,7 +802,7 @@ def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_
         rows * head_dim, _ptr(m), _ptr(out), _dtcode(out), B, n_heads, n_kv_heads, L, head_dim,
         float(scale_div), _ptr(part), _ptr(cnt), _stream(q))
     _check(rc, "qlin_attn_decode_rope")
-    return out
+    return part if partials_only else out
 
 
 def attn_prefill_supported(q, k, mask=None):

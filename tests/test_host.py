@@ -77,6 +77,18 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert gb(p, 256, p, 16, 0, p, 127, None, 0, p, 16, 2, 1, 16, 128, 4, 128, None) == 1  # x
     assert gb(p, 256, p, 16, 0, p, 128, p, 8, p, 16, 2, 1, 16, 128, 4, 128, None) == 1  # bias
     assert gb(p, 256, p, 16, 0, p, 128, None, 0, p, 16, 70000, 1, 16, 128, 4, 128, None) == 1
+    # ABI 9: the decode attention's split merge inside o_proj takes 2..10 splits, batch 1
+    assert lib.qlin_attn_decode_splits(1, 8, 40) == 1 and lib.qlin_attn_decode_splits(1, 8, 0) == -1
+    assert 2 <= lib.qlin_attn_decode_splits(1, 8, 513) <= 10
+    assert lib.qlin_attn_merge_linear_supported(513, 32, 8, 4096, 4, 128, 0) == 1
+    assert lib.qlin_attn_merge_linear_supported(40, 32, 8, 4096, 4, 128, 0) == 0    # one split
+    assert lib.qlin_attn_merge_linear_supported(4096, 32, 8, 4096, 4, 128, 0) == 0  # > 10 splits
+    assert lib.qlin_attn_merge_linear_supported(513, 32, 8, 4096, 4, 128, 8) == 0   # wide zeros
+    assert lib.qlin_attn_merge_linear_supported(513, 32, 8, 4096, 5, 128, 0) == 0   # bits
+    ml = lib.qlin_attn_merge_linear_f16
+    assert ml(None, 513, 32, 8, p, p, 0, None, p, p, 4096, 4, 128, None) == 1  # partials
+    assert ml(p, 513, 32, 8, p, p, 0, None, None, p, 4096, 4, 128, None) == 1  # residual
+    assert ml(p, 40, 32, 8, p, p, 0, None, p, p, 4096, 4, 128, None) == 1      # one split
     assert lib.qlin_gemm_block_cols(0, 16, 4) == -1 and lib.qlin_gemm_block_cols(16, 16, 5) == -1
     assert lib.qlin_error_string(1) == b"invalid argument"
 
