@@ -56,5 +56,8 @@ def run(B, Hq, Hkv, L, R=16, reps=20):
            "maxdiff_vs_first": diffs}, flush=True)
 
 
-for cfg in [(1, 32, 8, 513), (1, 32, 8, 2048), (1, 32, 8, 4096), (16, 32, 8, 2048), (64, 32, 8, 1024)][:int(os.environ.get("NCFG", "5"))]:
+CFGS = [(1, 32, 8, 513), (1, 32, 8, 2048), (1, 32, 8, 4096), (16, 32, 8, 2048), (64, 32, 8, 1024)]
+if os.environ.get("CFGS"):  # "B,Hq,Hkv,L;..."
+    CFGS = [tuple(int(x) for x in c.split(",")) for c in os.environ["CFGS"].split(";")]
+for cfg in CFGS[:int(os.environ.get("NCFG", "99"))]:
     run(*cfg)
