@@ -72,6 +72,7 @@ SIGNATURES = {
     "qlin_attn_decode_splits": ([_l, _i, _l], _i),
     "qlin_attn_merge_linear_supported": ([_l, _i, _i, _l, _i, _i, _i], _i),
     "qlin_attn_merge_linear_f16": ([_p, _l, _i, _i, _p, _p, _i, _p, _p, _p, _l, _i, _i, _p], _i),
+    "qlin_prefetch": ([_p, _l, _i, _p], _i),
     "qlin_decode_supported": ([_i, _l, _l, _i, _i, _i, _i, _i, _i], _i),
     "qlin_decode_workspace_bytes": ([_i, _l, _l, _i, _i, _i, _l], _l),
     "qlin_decode_llama_f16": ([_p, _i, _l, _l, _i, _i, _i, _i, _i, _i, ctypes.c_float, _p, _p, _p,
@@ -720,6 +721,17 @@ def _attn_partials(lib, device, B, Hq, Hkv, L, partials_only):
         return None, None
     part = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
     return part, (None if partials_only else _attn_counters(device, B * Hkv))
+
+
+def prefetch(*tensors, blocks=0):
+    """``qlin_prefetch`` (include/qlin_gfx950_prefetch.h): read each tensor once on the current
+    stream so it is cache-resident for a later launch (weights of the next linears, issued on a
+    side stream beside a latency-bound launch).  Changes no data."""
+    lib = load_library()
+    for t_ in tensors:
+        _dev(t_)
+        _check(lib.qlin_prefetch(_ptr(t_), t_.numel() * t_.element_size(), blocks, _stream(t_)),
+               "qlin_prefetch")
 
 
 def attn_merge_linear_supported(L, Hq, Hkv, N, bits, group, flags=0):

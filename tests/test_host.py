@@ -10,12 +10,16 @@ import torch
 from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "qlin_gfx950.h")
+HEADERS = sorted(os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))
+                 if f.endswith(".h"))
 
 
 def declared_symbols():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(qlin_\w+)\s*\(", src)))
+    syms = set()
+    for h in HEADERS:  # every include/*.h
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        syms.update(re.findall(r"\b(qlin_\w+)\s*\(", src))
+    return sorted(syms)
 
 
 def test_header_declares_the_abi():
@@ -89,6 +93,8 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert ml(None, 513, 32, 8, p, p, 0, None, p, p, 4096, 4, 128, None) == 1  # partials
     assert ml(p, 513, 32, 8, p, p, 0, None, None, p, 4096, 4, 128, None) == 1  # residual
     assert ml(p, 40, 32, 8, p, p, 0, None, p, p, 4096, 4, 128, None) == 1      # one split
+    assert lib.qlin_prefetch(None, 64, 0, None) == 1 and lib.qlin_prefetch(p, -1, 0, None) == 1
+    assert lib.qlin_prefetch(ctypes.c_void_p(8), 64, 0, None) == 1  # not 16-B aligned
     assert lib.qlin_gemm_block_cols(0, 16, 4) == -1 and lib.qlin_gemm_block_cols(16, 16, 5) == -1
     assert lib.qlin_error_string(1) == b"invalid argument"
 
