@@ -30,6 +30,7 @@
 #include "qlin_common.h"  // QLIN_OK / QLIN_EINVAL
 #include "qlin_gemv_tile.h"  // the packed-tile helpers of the merge + o_proj kernel
 #include "../../include/qlin_gfx950.h"
+#include "../../include/qlin_gfx950_prefetch.h"
 
 namespace {
 
@@ -109,6 +110,8 @@ struct RopeIn {
   int64_t pos_bs;
   _Float16* kc;  // the caches k / v (writable views of the same buffers)
   _Float16* vc;
+  const uint4* pf;  // qlin_attn_decode_rope_pf: bytes the extra blocks read (next launch's weights)
+  int64_t pf16;
 };
 
 template <int GRP, bool ROPE = false>
@@ -128,6 +131,24 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   __shared__ float ml_l[kMaxSplit][GRP];   // merge: chunk sums
   __shared__ int last;
 
+  if (ROPE && (int)blockIdx.y >= S) {  // a prefetch block (qlin_attn_decode_rope_pf)
+    const int64_t stride = (int64_t)(gridDim.y - S) * gridDim.x * kThreads;
+    const int64_t i0 = ((int64_t)(blockIdx.y - S) * gridDim.x + blockIdx.x) * kThreads + threadIdx.x;
+    uint32_t acc = 0;
+    for (int64_t i = i0; i < ri.pf16; i += 8 * stride) {
+      uint4 w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t j = i + u * stride;
+        w[u] = j < ri.pf16 ? ri.pf[j] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc ^= w[u].x ^ w[u].y ^ w[u].z ^ w[u].w;
+    }
+    // keeps the loads; never true for a real launch (L >= 1)
+    if (L == 0 && acc == 0x9E3779B9u) reinterpret_cast<uint32_t*>(out)[threadIdx.x] = acc;
+    return;
+  }
   const int bh = blockIdx.x;  // b * Hkv + kv head
   const int split = blockIdx.y;
   const int b = bh / Hkv, hk = bh % Hkv;
@@ -428,8 +449,8 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
 int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
                   void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int64_t kv_hs,
                   float scale_div, float* part_o, float* part_ml, int32_t* counters,
-                  const Split& sp, hipStream_t st, const RopeIn& ri) {
-  const dim3 grid((unsigned)(B * Hkv), (unsigned)sp.S);
+                  const Split& sp, hipStream_t st, const RopeIn& ri, int pf_y = 0) {
+  const dim3 grid((unsigned)(B * Hkv), (unsigned)(sp.S + pf_y));
   const int grp = Hq / Hkv;
 #define QLIN_A(G, R)                                                                          \
   hipLaunchKernelGGL((attn_decode_kernel<G, R>), grid, dim3(kThreads), 0, st, q,              \
@@ -490,7 +511,7 @@ extern "C" int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_
                        part_ml, counters, sp, (hipStream_t)stream, RopeIn{});
 }
 
-extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+static int attn_decode_rope_impl(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
                                      int64_t k_row_stride, const uint16_t* v,
                                      int64_t v_row_stride, const float* cos_cache,
                                      const float* sin_cache, int64_t cache_rows,
@@ -498,7 +519,8 @@ extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, co
                                      uint16_t* k_cache, uint16_t* v_cache, int64_t kv_head_stride,
                                      const uint16_t* mask, void* out, int out_dtype, int64_t B,
                                      int Hq, int Hkv, int64_t L, int D, float scale_div,
-                                     float* partials, int32_t* counters, void* stream) {
+                                     float* partials, int32_t* counters, void* stream,
+                                     const void* pf, int64_t pf_bytes, int pf_blocks) {
   // position_ids NULL: cos_cache / sin_cache are the rows of the step's position (B == 1)
   if (!position_ids && B > 1) return QLIN_EINVAL;
   if (!q || !k || !v || !cos_cache || !sin_cache || !k_cache || !v_cache ||
@@ -522,10 +544,43 @@ extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, co
   }
   const RopeIn ri{(const _Float16*)q, q_row_stride, (const _Float16*)k, k_row_stride,
                   (const _Float16*)v, v_row_stride, cos_cache, sin_cache, cache_rows,
-                  position_ids, pos_batch_stride, (_Float16*)k_cache, (_Float16*)v_cache};
+                  position_ids, pos_batch_stride, (_Float16*)k_cache, (_Float16*)v_cache,
+                  (const uint4*)pf, pf ? pf_bytes / 16 : 0};
+  const int pf_y = pf && pf_bytes >= 16 ? (int)((pf_blocks + heads - 1) / heads) : 0;
   return launch_decode(nullptr, k_cache, v_cache, mask, out, out_dtype, B, Hq, Hkv, L,
                        kv_head_stride, scale_div, part_o, part_ml, counters, sp,
-                       (hipStream_t)stream, ri);
+                       (hipStream_t)stream, ri, pf_y);
+}
+
+extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+                                     int64_t k_row_stride, const uint16_t* v,
+                                     int64_t v_row_stride, const float* cos_cache,
+                                     const float* sin_cache, int64_t cache_rows,
+                                     const int64_t* position_ids, int64_t pos_batch_stride,
+                                     uint16_t* k_cache, uint16_t* v_cache, int64_t kv_head_stride,
+                                     const uint16_t* mask, void* out, int out_dtype, int64_t B,
+                                     int Hq, int Hkv, int64_t L, int D, float scale_div,
+                                     float* partials, int32_t* counters, void* stream) {
+  return attn_decode_rope_impl(q, q_row_stride, k, k_row_stride, v, v_row_stride, cos_cache,
+                               sin_cache, cache_rows, position_ids, pos_batch_stride, k_cache,
+                               v_cache, kv_head_stride, mask, out, out_dtype, B, Hq, Hkv, L, D,
+                               scale_div, partials, counters, stream, nullptr, 0, 0);
+}
+
+extern "C" int qlin_attn_decode_rope_pf(
+    const uint16_t* q, int64_t q_row_stride, const uint16_t* k, int64_t k_row_stride,
+    const uint16_t* v, int64_t v_row_stride, const float* cos_cache, const float* sin_cache,
+    int64_t cache_rows, const int64_t* position_ids, int64_t pos_batch_stride, uint16_t* k_cache,
+    uint16_t* v_cache, int64_t kv_head_stride, const uint16_t* mask, void* out, int out_dtype,
+    int64_t B, int Hq, int Hkv, int64_t L, int D, float scale_div, float* partials,
+    int32_t* counters, void* stream, const void* pf, int64_t pf_bytes, int pf_blocks) {
+  if (!pf || pf_bytes < 16 || (reinterpret_cast<uintptr_t>(pf) & 15) || pf_blocks < 1 ||
+      pf_blocks > 4096)
+    return QLIN_EINVAL;
+  return attn_decode_rope_impl(q, q_row_stride, k, k_row_stride, v, v_row_stride, cos_cache,
+                               sin_cache, cache_rows, position_ids, pos_batch_stride, k_cache,
+                               v_cache, kv_head_stride, mask, out, out_dtype, B, Hq, Hkv, L, D,
+                               scale_div, partials, counters, stream, pf, pf_bytes, pf_blocks);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -44,6 +44,9 @@ def _side_stream(device):
 # down_proj's packed weights read beside the attention launch
 PREFETCH_DECODE_WEIGHTS = os.environ.get("QLIN_DECODE_PREFETCH", "0") != "0"
 PREFETCH_BLOCKS = int(os.environ.get("QLIN_DECODE_PREFETCH_BLOCKS", "0"))
+# opt-in: o_proj's packed weights read by extra blocks of the decode attention launch itself
+PREFETCH_O_IN_ATTN = os.environ.get("QLIN_ATTN_PREFETCH_O", "0") == "1"
+PREFETCH_O_BLOCKS = int(os.environ.get("QLIN_ATTN_PREFETCH_O_BLOCKS", "128"))
 
 
 def _rope_theta(config):
@@ -383,7 +386,10 @@ class QuantLlamaAttention(nn.Module):
                     q, k, v, cos_c, sin_c, position_ids, self.num_heads, self.num_key_value_heads,
                     self.head_dim, buf[0], buf[1], L0, attention_mask, math.sqrt(self.head_dim),
                     out_dtype=act_dtype if act_dtype == torch.float16 else torch.float32,
-                    partials_only=merge)
+                    partials_only=merge,
+                    prefetch=self.o_proj.qweight if PREFETCH_O_IN_ATTN and residual is not None
+                    and getattr(self.o_proj, "packed", False) else None,
+                    prefetch_blocks=PREFETCH_O_BLOCKS)
                 past_key_value = (buf[0][:, :, :L0 + 1], buf[1][:, :, :L0 + 1]) if use_cache else None
                 if merge:
                     # the split-L merge runs inside o_proj (+ residual): one launch fewer round

@@ -73,6 +73,9 @@ SIGNATURES = {
     "qlin_attn_merge_linear_supported": ([_l, _i, _i, _l, _i, _i, _i], _i),
     "qlin_attn_merge_linear_f16": ([_p, _l, _i, _i, _p, _p, _i, _p, _p, _p, _l, _i, _i, _p], _i),
     "qlin_prefetch": ([_p, _l, _i, _p], _i),
+    "qlin_attn_decode_rope_pf": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _p, _p,
+                                  _i, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p, _p, _l, _i],
+                                 _i),
     "qlin_decode_supported": ([_i, _l, _l, _i, _i, _i, _i, _i, _i], _i),
     "qlin_decode_workspace_bytes": ([_i, _l, _l, _i, _i, _i, _l], _l),
     "qlin_decode_llama_f16": ([_p, _i, _l, _l, _i, _i, _i, _i, _i, _i, ctypes.c_float, _p, _p, _p,
@@ -765,12 +768,14 @@ def attn_merge_linear(partials, L, Hq, Hkv, qweight, qsz, bias, residual, N, bit
 
 def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim,
                      k_cache, v_cache, kv0, mask, scale_div, out_dtype=torch.float32,
-                     partials_only=False):
+                     partials_only=False, prefetch=None, prefetch_blocks=128):
     """``qlin_attn_decode_rope``: ``rope_kv`` + ``attn_decode`` in one launch for one new token:
     q [B, 1, Hq*D], k / v [B, 1, Hkv*D] fp16 row-strided views (before RoPE); k_cache / v_cache
     fp16 [B, Hkv, rows, D] contiguous buffers holding rows 0 .. kv0 - 1, row kv0 written here;
     mask fp16 [B, 1, 1, kv0 + 1] or None -> [B, Hq, 1, D] (out_dtype), bit-identical to the two
-    launches.  partials_only: the split-L partials for ``attn_merge_linear`` instead."""
+    launches.  partials_only: the split-L partials for ``attn_merge_linear`` instead.
+    prefetch: a contiguous device tensor (the next launch's packed weights) read by
+    ``prefetch_blocks`` extra blocks of the same launch (``qlin_attn_decode_rope_pf``)."""
     for t_ in (q, k, v):
         if _rows(t_) is None:
             raise ValueError("attn_decode_rope takes row-strided [B, 1, H*D] q / k / v")
@@ -808,11 +813,17 @@ def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_
     lib = load_library()
     part, cnt = _attn_partials(lib, q.device, B, n_heads, n_kv_heads, L, partials_only)
     rows = k_cache.shape[2]
-    rc = lib.qlin_attn_decode_rope(
-        _ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(v), _rows(v), _ptr(cos_cache),
-        _ptr(sin_cache), cos_cache.shape[0], _ptr(pos), pbs, _ptr(k_cache), _ptr(v_cache),
-        rows * head_dim, _ptr(m), _ptr(out), _dtcode(out), B, n_heads, n_kv_heads, L, head_dim,
-        float(scale_div), _ptr(part), _ptr(cnt), _stream(q))
+    args = (_ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(v), _rows(v), _ptr(cos_cache),
+            _ptr(sin_cache), cos_cache.shape[0], _ptr(pos), pbs, _ptr(k_cache), _ptr(v_cache),
+            rows * head_dim, _ptr(m), _ptr(out), _dtcode(out), B, n_heads, n_kv_heads, L, head_dim,
+            float(scale_div), _ptr(part), _ptr(cnt), _stream(q))
+    if prefetch is not None:
+        _dev(prefetch)
+        rc = lib.qlin_attn_decode_rope_pf(*args, _ptr(prefetch),
+                                          prefetch.numel() * prefetch.element_size(),
+                                          prefetch_blocks)
+    else:
+        rc = lib.qlin_attn_decode_rope(*args)
     _check(rc, "qlin_attn_decode_rope")
     return part if partials_only else out
 

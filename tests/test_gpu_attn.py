@@ -230,6 +230,31 @@ def test_attn_merge_linear_rejects_unsupported():
         qlin.attn_decode(q, k, k, None, 8.0, partials_only=True)
 
 
+@pytest.mark.parametrize("kv0,blocks", [(512, 128), (40, 8), (300, 64)])
+def test_attn_decode_rope_prefetch_blocks_change_nothing(kv0, blocks):
+    """qlin_attn_decode_rope_pf: the extra prefetch blocks of the launch leave the attention output
+    and the written cache rows bit-identical."""
+    from models.int_llama_layer import LlamaRotaryEmbedding437
+    B, Hq, Hkv, D, rows = 1, 32, 8, 128, 1024
+    g = torch.Generator(device="cuda").manual_seed(kv0)
+    qkv = (torch.randn(B, 1, (Hq + 2 * Hkv) * D, device="cuda", generator=g) * 2).half()
+    q, k, v = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
+    rot = LlamaRotaryEmbedding437(D, 8192, 500000.0, device="cuda").half()
+    cos, sin = rot.cos_cached.float().contiguous(), rot.sin_cached.float().contiguous()
+    pos = torch.full((B, 1), kv0, device="cuda", dtype=torch.int64)
+    kc = torch.randn(B, Hkv, rows, D, device="cuda", generator=g).half()
+    vc = torch.randn(B, Hkv, rows, D, device="cuda", generator=g).half()
+    kc2, vc2 = kc.clone(), vc.clone()
+    w = torch.randint(-2**31, 2**31 - 1, (4096, 512), dtype=torch.int32, device="cuda")
+    a = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, kv0, None, math.sqrt(D),
+                              out_dtype=torch.float16)
+    b = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc2, vc2, kv0, None,
+                              math.sqrt(D), out_dtype=torch.float16, prefetch=w,
+                              prefetch_blocks=blocks)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(kc, kc2) and torch.equal(vc, vc2)
+
+
 def test_attn_decode_rejects_unsupported():
     q = torch.randn(1, 32, 1, 64, device="cuda")
     k = torch.randn(1, 8, 10, 64, device="cuda").half()

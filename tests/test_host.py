@@ -95,6 +95,9 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert ml(p, 40, 32, 8, p, p, 0, None, p, p, 4096, 4, 128, None) == 1      # one split
     assert lib.qlin_prefetch(None, 64, 0, None) == 1 and lib.qlin_prefetch(p, -1, 0, None) == 1
     assert lib.qlin_prefetch(ctypes.c_void_p(8), 64, 0, None) == 1  # not 16-B aligned
+    pf = lib.qlin_attn_decode_rope_pf
+    assert pf(None, 0, None, 0, None, 0, None, None, 0, None, 0, None, None, 0, None, None, 0,
+              1, 32, 8, 513, 128, 11.3, None, None, None, p, 64, 0) == 1  # no blocks
     assert lib.qlin_gemm_block_cols(0, 16, 4) == -1 and lib.qlin_gemm_block_cols(16, 16, 5) == -1
     assert lib.qlin_error_string(1) == b"invalid argument"
 
