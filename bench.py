@@ -105,8 +105,6 @@ def parse():
                     help="skip the decode-layer line (configs[1] inside the model, DESIGN.md §5)")
     ap.add_argument("--decode-layers", type=int, default=8)
     ap.add_argument("--decode-kv", type=int, default=512)
-    ap.add_argument("--decode-engine", action="store_true",
-                    help="also time the persistent one-launch decode engine")
     return ap.parse_args()
 
 
@@ -267,17 +265,6 @@ def decode_layer_bench(args, dev, timed):
     if pmc is not None:
         out["roofline"]["traffic"] = round(pmc["fetch_bytes_per_launch"])
         out["roofline"]["traffic_source"] = pmc["file"]
-    # the persistent one-launch engine over the same layers (opt-in)
-    if args.decode_engine:
-        from models.decode_engine import DecodeEngine
-        eng = DecodeEngine(layers)
-        if eng.reason is None:
-            with torch.no_grad():
-                eng_run = lambda: eng.step(x, pos, past, mask)  # noqa: E731
-                el_e, _ = timed(eng_run, steps, 2)
-            ue = el_e / steps / R * 1e6
-            out["engine"] = {"us_per_layer": round(ue, 2), "status": eng.status(),
-                             "frac": round(nbytes / ue / 1e3 / HBM_PEAK_GBS, 4)}
     del graph, layers
     torch.cuda.empty_cache()
     return out

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 9
+#define QLIN_ABI_VERSION 10
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -223,53 +223,21 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
  * RMSNorm + packed linear for ONE token row in one launch (the decoder layer's
  * input_layernorm -> fused q/k/v and post_attention_layernorm -> gate/up at decode; the norm is
  * OmniLlamaRMSNorm, quant/omni_norm.py:52-63 of the reference): x fp16 [K] is the hidden state
- * BEFORE the norm, norm_weight fp32 [K] (8-B aligned), eps its variance epsilon.  The GEMV
- * multiplies RN16(weight * x) (fp32 product, one fp16 rounding) and applies r = rsqrt(mean(x^2) +
- * eps) to the fp32 accumulators before F.linear's fp16 rounding: y = RN16(r * sum W_dq (w x)), then
- * `epilogue` as qlin_linear_ep_f16 — the norm's statistics (summed by the blocks from the x words
- * they load anyway) are needed only at the end, so the first MFMAs wait for nothing (round 3; the
- * round-2 form normalised x first, behind a barrier: 2 us more per decode layer).  The same
- * mathematics as the reference's RN16(w * (x * r)) with the fp16 rounding at another point:
- * outputs within a few fp16 ulps of the two launches (qlin_rmsnorm_f16, then the linear).  Supported: M == 1 on the fast GEMV path (K % 128 == 0,
- * group % 128 == 0 or group in {32, 64}, <= 4 weight tiles per wave) —
- * qlin_rmsnorm_linear_supported() says so (1) or not (0); otherwise QLIN_EINVAL.
+ * BEFORE the norm, norm_weight fp32 [K] (8-B aligned; the fp16 weight upcast, exact), eps its
+ * variance epsilon.  The kernel normalises x at the reference's rounding point,
+ * x_hat = RN16(weight * (x * rsqrt(mean(x^2) + eps))) with fp32 inside, and multiplies x_hat:
+ * y = F.linear(x_hat, W_dq, bias), then `epilogue` as qlin_linear_ep_f16.  The sum of squares runs
+ * in another order than torch's reduction (an fp32 ulp of the statistics can move an fp16 ulp of
+ * x_hat).  Supported: M == 1, K % 128 == 0, group % 128 == 0 or group in {32, 64}, and K / 128 =
+ * W * T with W <= 16 waves and T in {2, 4, 8} k-tiles per wave — qlin_rmsnorm_linear_supported()
+ * says so (1) or not (0); otherwise QLIN_EINVAL.
  */
 int qlin_rmsnorm_linear_supported(int64_t M, int64_t N, int64_t K, int bits, int group);
-/*
- * qlin_rmsnorm_linear_ep_f16 optional inputs (ABI 8), for the decode chain of a fused layer:
- *   sumsq_in / sumsq_n  precomputed statistics: sumsq_n == ceil(K / 16) partial sums of squares
- *                       of x, one per 16 consecutive elements, as qlin_linear_res_sumsq_f16 writes
- *                       them while producing x; r then comes from sum(partials) / K (a fixed
- *                       order) instead of the blocks' own sums.  NULL: computed in the kernel.
- *                       K <= 8192.  (Measured on the LLaMA3-8B decode layer: no gain over the
- *                       in-kernel sums since the late rsqrt; the fused layer does not use it.)
- *   rope_pos / rope_cos / rope_sin / rope_rows / rope_out  copy the RoPE cos and sin rows of
- *                       position rope_pos[0] (clamped to [0, rope_rows)) of the fp32 caches
- *                       [rope_rows][128] into rope_out[0..127] / [128..255] (16-B aligned), for a
- *                       following qlin_attn_decode_rope with position_ids NULL.  NULL: skipped.
- *                       (Measured: the attention launch is not shortened by it; unused by the
- *                       fused layer.)
- */
 int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                                const uint16_t* x, const float* norm_weight, float eps,
                                const uint16_t* bias, const uint16_t* residual, uint16_t* y,
                                int64_t M, int64_t N, int64_t K, int bits, int group, int epilogue,
-                               const float* sumsq_in, int64_t sumsq_n, const int64_t* rope_pos,
-                               const float* rope_cos, const float* rope_sin, int64_t rope_rows,
-                               float* rope_out, void* stream);
-
-/*
- * One token row: y[N] = RN16(residual + RN16(x @ W_dq^T + bias)) (QLIN_EP_RESIDUAL of
- * qlin_linear_ep_f16: o_proj / down_proj + the residual add, models/int_llama_layer.py:241-257)
- * that also writes sumsq_out[ceil(N / 16)]: per 16 consecutive outputs, the sum of the squares of
- * their fp16 values (fixed order) — the statistics of the RMSNorm that reads y next
- * (post_attention_layernorm / the next layer's input_layernorm, quant/omni_norm.py:52-63), for
- * qlin_rmsnorm_linear_ep_f16's sumsq_in.
- */
-int qlin_linear_res_sumsq_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
-                              const uint16_t* x, const uint16_t* bias, const uint16_t* residual,
-                              uint16_t* y, int64_t N, int64_t K, int bits, int group,
-                              float* sumsq_out, void* stream);
+                               void* stream);
 
 /*
  * Fused decode attention (one query token per sequence), for the quantized LLaMA layer's
@@ -286,11 +254,12 @@ int qlin_linear_res_sumsq_f16(const uint32_t* qweight, const uint32_t* qsz, int 
  * of `partials` scratch a call needs (0: none, pass NULL; -1: unsupported shapes); `counters` is
  * int32 [>= B * Hkv], zero-filled before its first use and left zero-filled by every call (the
  * merging block resets it), so one counter buffer serves all later calls on the same stream,
- * graph replays included; do not share it between streams running concurrently.  counters NULL
- * with partials (B == 1, qlin_attn_decode_splits() >= 2): the launch writes the split partials
- * only and `out` is left untouched — qlin_attn_merge_linear_f16 merges them inside o_proj.
+ * graph replays included; do not share it between streams running concurrently.
+ * qlin_attn_decode_splits(): the split count S of a (B, Hkv, L) launch (1: no partials, -1:
+ * unsupported arguments).
  */
 int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L);
+int qlin_attn_decode_splits(int64_t B, int Hkv, int64_t L);
 int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
                      void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int D,
                      int64_t kv_head_stride, float scale_div, float* partials, int32_t* counters,
@@ -304,8 +273,7 @@ int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_t* v, const
  * hold rows 0 .. L - 2 and receive the rotated k and the v row at L - 1 from this launch, which
  * then attends over all L rows (mask fp16 [B, L] or NULL).  Same arithmetic as the two launches
  * (bit-identical output and cache rows); partials / counters as qlin_attn_decode.  B == 1 may
- * pass position_ids NULL with cos / sin pointing at the step's own rows (e.g. the rope_out of
- * the q/k/v launch, qlin_rmsnorm_linear_ep_f16): no position -> row round trip in this launch.
+ * pass position_ids NULL with cos / sin pointing at the step's own rows.
  */
 int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
                           int64_t k_row_stride, const uint16_t* v, int64_t v_row_stride,
@@ -314,27 +282,6 @@ int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_
                           uint16_t* v_cache, int64_t kv_head_stride, const uint16_t* mask,
                           void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int D,
                           float scale_div, float* partials, int32_t* counters, void* stream);
-
-/*
- * The split-L partials of a decode attention launch (qlin_attn_decode / _rope with counters NULL,
- * B == 1) merged inside o_proj: y = residual + F.linear(attn, W, bias) with attn = the attention
- * output rounded to fp16 (the layer's .to(fp16)), i.e. qlin_attn_decode(out_dtype QLIN_F16)
- * followed by qlin_linear_ep_f16(QLIN_EP_RESIDUAL) in one launch — same arithmetic up to the fp32
- * summation order of the merge.  Replaces the reference's o_proj(attn_output) and the residual
- * add after it (models/int_llama_layer.py:174, :249) for one decode token.
- *   partials  as written by the attention launch for (B = 1, Hq, Hkv, L);  qweight / qsz / flags /
- *   bias / bits / group  the packed o_proj [N, Hq * 128] (narrow or float zeros);  residual, y
- *   fp16 [N].  qlin_attn_decode_splits(): the split count S of a (B, Hkv, L) launch (1: no
- *   partials, -1: unsupported); qlin_attn_merge_linear_supported(): 1 when this entry takes the
- *   shape (2 <= S <= 10, Hq <= 64 heads).
- */
-int qlin_attn_decode_splits(int64_t B, int Hkv, int64_t L);
-int qlin_attn_merge_linear_supported(int64_t L, int Hq, int Hkv, int64_t N, int bits, int group,
-                                     int flags);
-int qlin_attn_merge_linear_f16(const float* partials, int64_t L, int Hq, int Hkv,
-                               const uint32_t* qweight, const uint32_t* qsz, int flags,
-                               const uint16_t* bias, const uint16_t* residual, uint16_t* y,
-                               int64_t N, int bits, int group, void* stream);
 
 /*
  * Fused prefill attention (many query tokens per sequence): the same attention core as
@@ -414,56 +361,6 @@ int qlin_rope_kv_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
 int qlin_attn_scores_f32(float* scores, const void* mask, int mask_dtype, int64_t B, int64_t H,
                          int64_t T, int64_t L, int64_t mask_batch_stride, float scale_div,
                          void* stream);
-
-/*
- * Persistent decode engine: ONE launch runs one decode step — batch 1, one new token over a KV
- * cache — through n_layers consecutive quantized LLaMA decoder layers.  Replaces, per layer,
- * QuantLlamaDecoderLayer.forward at q_len == 1 (models/int_llama_layer.py:213-267 of the
- * reference: RMSNorm, q/k/v QuantLinear, RoPE, KV append, attention, o_proj + residual, RMSNorm,
- * gate/up QuantLinear + SiLU * up, down_proj + residual; every QuantLinear.forward =
- * F.linear(x, W_dq), quant/int_linear.py:62).  Every CU streams its share of all the layers'
- * packed weights continuously; the activations cross CUs through agent-scope hand-offs inside the
- * launch (DESIGN.md §4 "decode engine").
- *   layers  DEVICE array of n_layers qlin_decode_layer (the packed operands of each layer, all
- *           with the same bits / group / flags; q/k/v rows concatenated as FusedPackedLinear,
- *           gate/up interleaved in 8-row halves as qlin_linear_ep_f16's QLIN_EP_SILU_MUL layout);
- *   x       fp16 [H] the first layer's input hidden state;  y  fp16 [H] the last layer's output;
- *   caches  fp16 [Hkv, kv_rows, D] per layer, rows 0 .. L0 - 1 valid; the step writes the rotated k
- *           and the v row at L0 and attends over L0 + 1 rows;
- *   cos_cache, sin_cache  fp32 [cache_rows, D], position  int64 device scalar (as qlin_rope_f16);
- *   mask    fp16 [L0 + 1] additive or NULL;  scale_div = sqrt(D);  eps  the RMSNorms' epsilon;
- *   workspace  >= qlin_decode_workspace_bytes(n_layers, H, I, Hq, Hkv, D, L0 + 1) bytes, 256-B
- *           aligned, owned by the caller, used by one launch at a time; its first int32 is 0 after
- *           a completed step and nonzero if a cross-CU wait timed out (every wave then exits; y is
- *           undefined) — the caller may read it back to check.
- * Arithmetic: the GEMV tiles of qlin_gemv_f16 (exact W_dq, fp32 accumulation, fp16 outputs, the
- * fp16 epilogues); a row whose k-tiles are split over waves is summed in k order; RMSNorm and
- * attention as qlin_rmsnorm_linear_ep_f16 / qlin_attn_decode_rope (fp32).  Equal to the per-layer
- * launches up to fp32 summation order.  Requires D == 128, Hq == H / D, Hq / Hkv <= 8,
- * H <= 8192, I <= 16384 (both multiples of 128), L0 + 1 <= 4096, group a multiple of 128 or 64,
- * no QLIN_WIDE_ZERO, and enough CUs that every phase has <= 8 tile rows per CU
- * (qlin_decode_supported); every CU runs one 512-thread workgroup of the launch, so nothing else
- * may occupy the device's CUs while it runs.
- */
-typedef struct qlin_decode_layer {
-  const uint32_t* qweight[4]; /* q/k/v (fused), o_proj, gate/up (interleaved), down_proj */
-  const uint32_t* qsz[4];
-  const float* input_norm;    /* fp32 [H] RMSNorm weights */
-  const float* post_norm;
-  uint16_t* k_cache;          /* fp16 [Hkv, kv_rows, D] */
-  uint16_t* v_cache;
-} qlin_decode_layer;
-
-int qlin_decode_supported(int n_layers, int64_t H, int64_t I, int Hq, int Hkv, int D, int bits,
-                          int group, int flags);
-int64_t qlin_decode_workspace_bytes(int n_layers, int64_t H, int64_t I, int Hq, int Hkv, int D,
-                                    int64_t max_L);
-int qlin_decode_llama_f16(const void* layers, int n_layers, int64_t H, int64_t I, int Hq,
-                          int Hkv, int D, int bits, int group, int flags, float eps,
-                          const uint16_t* x, uint16_t* y, const float* cos_cache,
-                          const float* sin_cache, int64_t cache_rows, const int64_t* position,
-                          int64_t L0, int64_t kv_rows, const uint16_t* mask, float scale_div,
-                          void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,9 +28,7 @@
 // and sums run in a different order than hipBLASLt's bmm and the softmax is merged across chunks
 // (exp(m_c - M) rescaling), so results agree with the reference to fp32 rounding, not bit for bit.
 #include "qlin_common.h"  // QLIN_OK / QLIN_EINVAL
-#include "qlin_gemv_tile.h"  // the packed-tile helpers of the merge + o_proj kernel
 #include "../../include/qlin_gfx950.h"
-#include "../../include/qlin_gfx950_prefetch.h"
 
 namespace {
 
@@ -110,8 +108,6 @@ struct RopeIn {
   int64_t pos_bs;
   _Float16* kc;  // the caches k / v (writable views of the same buffers)
   _Float16* vc;
-  const uint4* pf;  // qlin_attn_decode_rope_pf: bytes the extra blocks read (next launch's weights)
-  int64_t pf16;
 };
 
 template <int GRP, bool ROPE = false>
@@ -131,24 +127,6 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   __shared__ float ml_l[kMaxSplit][GRP];   // merge: chunk sums
   __shared__ int last;
 
-  if (ROPE && (int)blockIdx.y >= S) {  // a prefetch block (qlin_attn_decode_rope_pf)
-    const int64_t stride = (int64_t)(gridDim.y - S) * gridDim.x * kThreads;
-    const int64_t i0 = ((int64_t)(blockIdx.y - S) * gridDim.x + blockIdx.x) * kThreads + threadIdx.x;
-    uint32_t acc = 0;
-    for (int64_t i = i0; i < ri.pf16; i += 8 * stride) {
-      uint4 w[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int64_t j = i + u * stride;
-        w[u] = j < ri.pf16 ? ri.pf[j] : make_uint4(0u, 0u, 0u, 0u);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc ^= w[u].x ^ w[u].y ^ w[u].z ^ w[u].w;
-    }
-    // keeps the loads; never true for a real launch (L >= 1)
-    if (L == 0 && acc == 0x9E3779B9u) reinterpret_cast<uint32_t*>(out)[threadIdx.x] = acc;
-    return;
-  }
   const int bh = blockIdx.x;  // b * Hkv + kv head
   const int split = blockIdx.y;
   const int b = bh / Hkv, hk = bh % Hkv;
@@ -352,9 +330,6 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
     float* ml = part_ml + ((int64_t)bh * S + split) * GRP * 2;
     part_store(ml + tid, (tid & 1) ? cl[tid >> 1] : cm[tid >> 1]);
   }
-  // counters NULL: partials only — the merge runs in the consumer (qlin_attn_merge_linear_f16,
-  // o_proj), and this launch ends after the stores (no drain, count or merge round trips here)
-  if (!counters) return;
 #if ATTN_FENCE_MODE == 0
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sc1 stores acknowledged before the count
 #else
@@ -449,8 +424,8 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
 int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
                   void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int64_t kv_hs,
                   float scale_div, float* part_o, float* part_ml, int32_t* counters,
-                  const Split& sp, hipStream_t st, const RopeIn& ri, int pf_y = 0) {
-  const dim3 grid((unsigned)(B * Hkv), (unsigned)(sp.S + pf_y));
+                  const Split& sp, hipStream_t st, const RopeIn& ri) {
+  const dim3 grid((unsigned)(B * Hkv), (unsigned)sp.S);
   const int grp = Hq / Hkv;
 #define QLIN_A(G, R)                                                                          \
   hipLaunchKernelGGL((attn_decode_kernel<G, R>), grid, dim3(kThreads), 0, st, q,              \
@@ -503,7 +478,7 @@ extern "C" int qlin_attn_decode(const float* q, const uint16_t* k, const uint16_
   const int64_t heads = B * Hkv;
   float *part_o = nullptr, *part_ml = nullptr;
   if (sp.S > 1) {
-    if (!partials) return QLIN_EINVAL;  // counters NULL: partials only (qlin_attn_merge_linear_f16)
+    if (!partials || !counters) return QLIN_EINVAL;
     part_o = partials;
     part_ml = part_o + heads * sp.S * grp * kD;
   }
@@ -519,8 +494,7 @@ static int attn_decode_rope_impl(const uint16_t* q, int64_t q_row_stride, const 
                                      uint16_t* k_cache, uint16_t* v_cache, int64_t kv_head_stride,
                                      const uint16_t* mask, void* out, int out_dtype, int64_t B,
                                      int Hq, int Hkv, int64_t L, int D, float scale_div,
-                                     float* partials, int32_t* counters, void* stream,
-                                     const void* pf, int64_t pf_bytes, int pf_blocks) {
+                                     float* partials, int32_t* counters, void* stream) {
   // position_ids NULL: cos_cache / sin_cache are the rows of the step's position (B == 1)
   if (!position_ids && B > 1) return QLIN_EINVAL;
   if (!q || !k || !v || !cos_cache || !sin_cache || !k_cache || !v_cache ||
@@ -538,18 +512,16 @@ static int attn_decode_rope_impl(const uint16_t* q, int64_t q_row_stride, const 
   const int64_t heads = B * Hkv;
   float *part_o = nullptr, *part_ml = nullptr;
   if (sp.S > 1) {
-    if (!partials) return QLIN_EINVAL;  // counters NULL: partials only (qlin_attn_merge_linear_f16)
+    if (!partials || !counters) return QLIN_EINVAL;
     part_o = partials;
     part_ml = part_o + heads * sp.S * grp * kD;
   }
   const RopeIn ri{(const _Float16*)q, q_row_stride, (const _Float16*)k, k_row_stride,
                   (const _Float16*)v, v_row_stride, cos_cache, sin_cache, cache_rows,
-                  position_ids, pos_batch_stride, (_Float16*)k_cache, (_Float16*)v_cache,
-                  (const uint4*)pf, pf ? pf_bytes / 16 : 0};
-  const int pf_y = pf && pf_bytes >= 16 ? (int)((pf_blocks + heads - 1) / heads) : 0;
+                  position_ids, pos_batch_stride, (_Float16*)k_cache, (_Float16*)v_cache};
   return launch_decode(nullptr, k_cache, v_cache, mask, out, out_dtype, B, Hq, Hkv, L,
                        kv_head_stride, scale_div, part_o, part_ml, counters, sp,
-                       (hipStream_t)stream, ri, pf_y);
+                       (hipStream_t)stream, ri);
 }
 
 extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
@@ -564,246 +536,10 @@ extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, co
   return attn_decode_rope_impl(q, q_row_stride, k, k_row_stride, v, v_row_stride, cos_cache,
                                sin_cache, cache_rows, position_ids, pos_batch_stride, k_cache,
                                v_cache, kv_head_stride, mask, out, out_dtype, B, Hq, Hkv, L, D,
-                               scale_div, partials, counters, stream, nullptr, 0, 0);
+                               scale_div, partials, counters, stream);
 }
-
-extern "C" int qlin_attn_decode_rope_pf(
-    const uint16_t* q, int64_t q_row_stride, const uint16_t* k, int64_t k_row_stride,
-    const uint16_t* v, int64_t v_row_stride, const float* cos_cache, const float* sin_cache,
-    int64_t cache_rows, const int64_t* position_ids, int64_t pos_batch_stride, uint16_t* k_cache,
-    uint16_t* v_cache, int64_t kv_head_stride, const uint16_t* mask, void* out, int out_dtype,
-    int64_t B, int Hq, int Hkv, int64_t L, int D, float scale_div, float* partials,
-    int32_t* counters, void* stream, const void* pf, int64_t pf_bytes, int pf_blocks) {
-  if (!pf || pf_bytes < 16 || (reinterpret_cast<uintptr_t>(pf) & 15) || pf_blocks < 1 ||
-      pf_blocks > 4096)
-    return QLIN_EINVAL;
-  return attn_decode_rope_impl(q, q_row_stride, k, k_row_stride, v, v_row_stride, cos_cache,
-                               sin_cache, cache_rows, position_ids, pos_batch_stride, k_cache,
-                               v_cache, kv_head_stride, mask, out, out_dtype, B, Hq, Hkv, L, D,
-                               scale_div, partials, counters, stream, pf, pf_bytes, pf_blocks);
-}
-
-// ---------------------------------------------------------------------------------------------
-// The split-L merge fused into o_proj (decode, batch 1).  The attention launch writes its S
-// chunk partials only (counters NULL above), and this launch — the o_proj GEMV with the residual
-// epilogue (qlin_linear_ep_f16 QLIN_EP_RESIDUAL, the decoder layer's residual + o_proj(attn),
-// models/int_llama_layer.py:174, :249 of the reference) — forms each x word from them while
-// its weight tiles stream: tile kt of the o_proj input is query head kt (head_dim 128 = one
-// k-tile), lane l merges elements 2l, 2l + 1 of that head: x = RN16(sum_s w_s o_s / sum_s w_s l_s),
-// w_s = exp(m_s - max m), the attention output rounded to fp16 as the layer's .to(fp16).  The
-// partial loads go out with the code loads (one round trip, L2-resident), so the merge costs the
-// GEMV little while the attention launch loses its drain / count / merge round trips
-// (tools/dev/attn_ab.py: 8.9 -> 5.9 us at L = 513 without them).  Same mathematics as the
-// attention launch's own merge, other fp32 summation order.
-// ---------------------------------------------------------------------------------------------
-namespace {
-
-constexpr int kMergeMaxS = 10;  // partials merged per x word (L <= 640 with 64-key chunks)
-constexpr int kMergeMaxW = 16;  // waves per block
-
-struct MergeArgs {
-  const float* part_o;   // [Hkv][S][grp][128]
-  const float* part_ml;  // [Hkv][S][grp][2]
-  int S, grp;
-  const uint32_t* qw;    // o_proj row tile 0
-  const uint32_t* qsz;
-  const _Float16* bias;
-  const _Float16* res;
-  _Float16* y;
-  int N, Kt, G, W, lw;
-  uint32_t cmagic;       // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
-};
-
-template <int BITS, int GPT, int ZM, int PF>
-__global__ __launch_bounds__(64 * kMergeMaxW) void attn_merge_linear_kernel(const MergeArgs a) {
-  __shared__ __attribute__((aligned(16))) float red[kTileN * kMergeMaxW];
-  __shared__ __attribute__((aligned(16))) uint32_t xs[kMergeMaxW][64];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63, n_in = lane & 15;
-  const int nt = blockIdx.x;
-  const uint32_t* qw = a.qw + (int64_t)nt * a.Kt * (64 * BITS) + lane * BITS;
-  const uint32_t* sz = a.qsz + (int64_t)nt * a.G * kTileN + n_in;
-  const int nts = (a.Kt - wave + a.W - 1) >> a.lw;  // >= 1: W <= Kt
-  const int ktl = wave + ((nts - 1) << a.lw);
-  auto kt_of = [&](int i) { return min(wave + (i << a.lw), ktl); };
-  auto group_of_tile = [&](int kt) {
-    return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
-  };
-  WTile<BITS, GPT> wt[PF];
-  float2 po[PF][kMergeMaxS];  // this lane's two elements of every partial of the tile's head
-  float2 ml[PF][kMergeMaxS];  // (max, sum) of every partial (the same for all lanes)
-#pragma unroll
-  for (int u = 0; u < PF; ++u) wt[u].pc = load_piece_nt<BITS>(qw + kt_of(u) * (64 * BITS));
-#pragma unroll
-  for (int u = 0; u < PF; ++u) {
-    const int kt = kt_of(u);
-    const int g0 = group_of_tile(kt);
-#pragma unroll
-    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = sz[(g0 + s) * kTileN];
-    const int hk = kt / a.grp, g = kt - hk * a.grp;  // query head kt = KV head hk, member g
-    const float* pob = a.part_o + ((int64_t)hk * a.S * a.grp + g) * kD + 2 * lane;
-    const float* pmb = a.part_ml + ((int64_t)hk * a.S * a.grp + g) * 2;
-#pragma unroll
-    for (int s = 0; s < kMergeMaxS; ++s) {
-      const int sc = min(s, a.S - 1);
-      po[u][s] = *reinterpret_cast<const float2*>(pob + (int64_t)sc * a.grp * kD);
-      ml[u][s] = *reinterpret_cast<const float2*>(pmb + (int64_t)sc * a.grp * 2);
-    }
-  }
-  // the epilogue's bias / residual operands (wave 0's lanes 0..15), fetched while the rest flies
-  const int64_t orow = (int64_t)nt * kTileN + min(tid, kTileN - 1);
-  const _Float16 ob = a.bias ? a.bias[min(orow, (int64_t)a.N - 1)] : (_Float16)0;
-  const _Float16 ores = a.res[min(orow, (int64_t)a.N - 1)];
-
-  const Magics mg = make_magics<BITS>();
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  uint32_t* slot = &xs[wave][0];
-  auto tile = [&](int u) {
-    // merged x words of this lane (query head kt_of(u), elements 2 lane, 2 lane + 1)
-    float M = ml[u][0].x;
-#pragma unroll
-    for (int s = 1; s < kMergeMaxS; ++s)
-      if (s < a.S) M = fmaxf(M, ml[u][s].x);
-    float den = 0.f, x0 = 0.f, x1 = 0.f;
-#pragma unroll
-    for (int s = 0; s < kMergeMaxS; ++s) {
-      if (s < a.S) {
-        const float w = expf(ml[u][s].x - M);
-        den = fmaf(w, ml[u][s].y, den);
-        x0 = fmaf(w, po[u][s].x, x0);
-        x1 = fmaf(w, po[u][s].y, x1);
-      }
-    }
-    // the attention output as the layer hands it to o_proj: fp32 / den, rounded once to fp16; a
-    // slot past the wave's tiles (a repeat of its last tile) multiplies zeros
-    const bool live = u < nts;
-    XRaw<1> xr;
-    xr.w[0] = live ? as_u32(h2{(_Float16)(x0 / den), (_Float16)(x1 / den)}) : 0u;
-    h8 xa[4];
-    park_x<1>(xa, xr, slot, lane, n_in);
-    auto step = [&](auto S_) {
-      constexpr int S = decltype(S_)::value;
-      uint32_t v[4];
-      const GroupQ gq = make_group_w<BITS, ZM>(wt[u].sz[S * GPT / 4]);
-      dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
-      const h8 b = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], b, acc, 0, 0, 0);
-    };
-    step(std::integral_constant<int, 0>{});
-    step(std::integral_constant<int, 1>{});
-    step(std::integral_constant<int, 2>{});
-    step(std::integral_constant<int, 3>{});
-  };
-#pragma unroll
-  for (int u = 0; u < PF; ++u) tile(u);
-  // combine the W partial rows: C row 0 sits in lanes 0..15 (element 0)
-  if (lane < kTileN) red[lane * kMergeMaxW + wave] = acc[0];
-  if (wave == 0 && lane < kTileN)
-    for (int w = a.W; w < kMergeMaxW; ++w) red[lane * kMergeMaxW + w] = 0.f;
-  __syncthreads();
-  if (tid < kTileN && orow < a.N) {
-    const f4* r = reinterpret_cast<const f4*>(red + tid * kMergeMaxW);
-    const f4 p = r[0], q = r[1], c = r[2], d = r[3];
-    const f4 e = (p + q) + (c + d);
-    float t = (e[0] + e[1]) + (e[2] + e[3]);
-    if (a.bias) t += (float)ob;
-    t = (float)(_Float16)t;                     // F.linear's fp16 output
-    a.y[orow] = (_Float16)((float)ores + t);    // + the residual, one fp16 rounding
-  }
-}
-
-// geometry: waves (a power of two <= 16) so that every wave streams <= 4 tiles
-bool merge_geometry(int Kt, int& W, int& lw, int& pf) {
-  W = 1;
-  lw = 0;
-  while (2 * W <= kMergeMaxW && 2 * W <= Kt) {
-    W *= 2;
-    ++lw;
-  }
-  const int tpw = (Kt + W - 1) / W;
-  if (tpw > 4) return false;
-  pf = tpw <= 2 ? 2 : 4;
-  return true;
-}
-
-bool merge_ok(int64_t L, int Hq, int Hkv, int64_t N, int bits, int group, int flags, Split& sp,
-              int& W, int& lw, int& pf) {
-  if (L < 1 || L > kMaxL || Hq <= 0 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > kMaxGroup || N < 1 ||
-      N > (1 << 30) || !(bits == 2 || bits == 3 || bits == 4 || bits == 8))
-    return false;
-  const int64_t K = (int64_t)Hq * kD;
-  if (!valid_layout(N, K, bits, group) || !(group % kTileK == 0 || group == 64)) return false;
-  if (zero_mode(flags) == kZWide) return false;
-  sp = choose_split(1, Hkv, L);
-  if (sp.S < 2 || sp.S > kMergeMaxS) return false;
-  return merge_geometry(Hq, W, lw, pf);
-}
-
-}  // namespace
 
 extern "C" int qlin_attn_decode_splits(int64_t B, int Hkv, int64_t L) {
   if (B < 1 || Hkv < 1 || L < 1 || L > kMaxL) return -1;
   return choose_split(B, Hkv, L).S;
-}
-
-extern "C" int qlin_attn_merge_linear_supported(int64_t L, int Hq, int Hkv, int64_t N, int bits,
-                                                int group, int flags) {
-  Split sp;
-  int W, lw, pf;
-  return merge_ok(L, Hq, Hkv, N, bits, group, flags, sp, W, lw, pf) ? 1 : 0;
-}
-
-extern "C" int qlin_attn_merge_linear_f16(const float* partials, int64_t L, int Hq, int Hkv,
-                                          const uint32_t* qweight, const uint32_t* qsz,
-                                          int flags, const uint16_t* bias,
-                                          const uint16_t* residual, uint16_t* y, int64_t N,
-                                          int bits, int group, void* stream) {
-  Split sp;
-  int W = 0, lw = 0, pf = 0;
-  if (!partials || !qweight || !qsz || !residual || !y ||
-      !merge_ok(L, Hq, Hkv, N, bits, group, flags, sp, W, lw, pf))
-    return QLIN_EINVAL;
-  const int grp = Hq / Hkv;
-  MergeArgs a;
-  a.part_o = partials;
-  a.part_ml = partials + (int64_t)Hkv * sp.S * grp * kD;
-  a.S = sp.S;
-  a.grp = grp;
-  a.qw = qweight;
-  a.qsz = qsz;
-  a.bias = (const _Float16*)bias;
-  a.res = (const _Float16*)residual;
-  a.y = (_Float16*)y;
-  a.N = (int)N;
-  a.Kt = Hq;  // K = Hq * 128
-  a.G = (int)((int64_t)Hq * kD / group);
-  a.W = W;
-  a.lw = lw;
-  const uint64_t c = group % kTileK == 0 ? (uint64_t)(group / kTileK) : 1;
-  a.cmagic = (uint32_t)(((1ull << 31) + c - 1) / c);
-  hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((unsigned)((N + kTileN - 1) / kTileN));
-  const int zm = zero_mode(flags);
-#define QLIN_MK(B, GP, Z)                                                                     \
-  if (pf == 2) hipLaunchKernelGGL((attn_merge_linear_kernel<B, GP, Z, 2>), grid, dim3(64 * W), \
-                                  0, st, a);                                                 \
-  else hipLaunchKernelGGL((attn_merge_linear_kernel<B, GP, Z, 4>), grid, dim3(64 * W), 0, st, a)
-#define QLIN_MG(B, Z)                                   \
-  if (group % kTileK == 0) { QLIN_MK(B, 1, Z); }        \
-  else { QLIN_MK(B, 2, Z); }
-#define QLIN_MB(B)                                      \
-  if (zm == kZFloat) { QLIN_MG(B, kZFloat); }           \
-  else { QLIN_MG(B, kZNarrow); }                        \
-  break
-  switch (bits) {
-    case 2: QLIN_MB(2);
-    case 3: QLIN_MB(3);
-    case 4: QLIN_MB(4);
-    default: QLIN_MB(8);
-  }
-#undef QLIN_MB
-#undef QLIN_MG
-#undef QLIN_MK
-  return (int)hipGetLastError();
 }

@@ -373,12 +373,10 @@ constexpr int kEpSiluMul = 2;
 
 // the GEMV kernel with an output epilogue (qlin_gemv.hip), for qlin_linear_ep_f16
 // (act_bits != 0: per-token activation fake-quant of x with the quantizer flags act_flags)
-// sq_out (M == 1, QLIN_EP_RESIDUAL only): per 16-row output tile, the sum of squares of its fp16
-// outputs (fixed order) -> sq_out[tile]: the next RMSNorm's statistics, precomputed
 int gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
             const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M, int64_t N,
             int64_t K, int bits, int group, int epilogue, int act_bits, int act_flags,
-            void* stream, float* sq_out = nullptr);
+            void* stream);
 
 // CUs of the current device, cached per device id (qlin_gemm.hip; used by the GEMM's block-width
 // picker and the batched GEMV's resident-grid size)

@@ -35,7 +35,7 @@
 
 using namespace qlin;
 
-namespace {
+namespace qlin_gv {
 
 constexpr int kMaxWaves = 16;
 
@@ -52,7 +52,6 @@ struct Ep {  // output epilogue (qlin_common.h kEp*) and fused activation fake-q
   const uint16_t* res;
   int ep;
   ActQ aq;
-  float* sq_out = nullptr;  // M == 1, kEpResidual: per-tile sums of squares of y
 };
 
 struct Geo {
@@ -201,24 +200,12 @@ __device__ __forceinline__ void gemv_body(const Geo& g, uint32_t* xslot, int kt0
 
 }
 
-// the sum of squares of the 16 outputs one tile row's block writes (lanes 0..15 of wave 0 hold
-// them; every other lane 0) in a fixed butterfly order -> sq_out[nt]: the statistics of the
-// RMSNorm that reads this output next (qlin_rmsnorm_linear_ep_f16's sumsq_in), precomputed
-__device__ __forceinline__ void sq_tile_out(float v, float* sq_out, int64_t nt) {
-#pragma clang fp contract(off)
-  v = v + __shfl_xor(v, 8);
-  v = v + __shfl_xor(v, 4);
-  v = v + __shfl_xor(v, 2);
-  v = v + __shfl_xor(v, 1);
-  if ((threadIdx.x & 63) == 0) sq_out[nt] = v;
-}
-
 template <int BITS, int MT, int GPT, int ZM, int PF, int NTB = 1>
 __global__ __launch_bounds__(1024) void gemv_kernel(
     const uint32_t* __restrict__ qw, const uint32_t* __restrict__ qsz,
     const _Float16* __restrict__ x, const _Float16* __restrict__ bias, _Float16* __restrict__ y,
     int M, int N, int K, int group, uint32_t gmagic, int tpw, const _Float16* __restrict__ res,
-    int ep, ActQ aq, float* __restrict__ sq_out) {
+    int ep, ActQ aq) {
   __shared__ __attribute__((aligned(16))) float red[NTB * MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
   __shared__ float aq_s[2][MT];
@@ -337,7 +324,6 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
     }
     return;
   }
-  float sqv = 0.f;  // sq_out: this thread's output squared
   for (int o = tid; o < NTB * MT * kTileN; o += blockDim.x) {
     const int j = o / (MT * kTileN), oo = o - j * MT * kTileN;
     const int m = oo / kTileN, n = oo - m * kTileN;
@@ -346,44 +332,256 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
       float t = total(o, row);
       if (ep == kEpResidual) t += (float)res[(int64_t)m * N + row];
       y[(int64_t)m * N + row] = (_Float16)t;
-      const float f = (float)(_Float16)t;
-      sqv = f * f;
     }
   }
-  if (sq_out && wave == 0) sq_tile_out(sqv, sq_out, nt);  // M == 1, NTB == 1 (host)
 }
 
 // ---------------------------------------------------------------------------------------------
-// Decode fast path: M <= 4, K % 128 == 0, group % 128 == 0 or group in {32, 64}, no activation
-// fake-quant.  Same arithmetic as gemv_kernel (exact W_dq, one MFMA per k-step), built for the
-// ~3-4 us a 4096 x 4096 launch lasts (tools/dev/gemv_lab2.hip, gemv_lab3.hip):
-//   - everything the general kernel derives by integer division (tiles, groups, strides) comes
-//     precomputed from the host, so the first weight load issues a few scalar ops after the
-//     kernel arguments land; the epilogue is a template parameter, so the executed code is one
-//     short straight line (the weights arrive ~1 us after the start: code fetched late, or work
-//     queued in front of the loads, shows up 1:1 in the launch time);
-//   - wave w streams tiles kt = w, w + W, w + 2W, ...: the tiles in flight on a CU at one time
-//     are W tiles (W x 1 KB for int4) apart in HBM instead of adjacent (4096^2: 3.89 -> 3.74 us);
-//   - all codes of the prefetch window are issued before their (scale, zero) words and x, so the
-//     first tile only waits for its own three loads.
+// Decode path, one token row (M == 1): the persistent "rows" kernel.
+//
+// QuantLinear.forward -> F.linear(x, W_dq) (quant/int_linear.py:62 of the reference) for one
+// token, optionally with the decoder layer's RMSNorm in front (OmniLlamaRMSNorm,
+// quant/omni_norm.py:52-63: input_layernorm -> q/k/v, post_attention_layernorm -> gate/up) and
+// its glue behind (residual add, SiLU * up; models/int_llama_layer.py:44-45, :241-257).
+//
+// Decomposition (the single-launch analogue of the batched streaming kernel,
+// qlin_gemv_batched.hip): block b owns the 16-row tile rows b, b + nb, b + 2 nb, ...; its W waves
+// split K, wave w taking the same TPW k-tiles of every row (W * TPW == Kt).  A wave therefore
+// loads its x words ONCE per launch (parked in its LDS slots, read back as MFMA A fragments for
+// every row) and streams its weight tiles row after row with PF tiles in flight across row
+// boundaries: no block ever waits between rows, and a grid of one block per CU keeps every CU
+// streaming until the matrix is done (gate/up, 1,792 tile rows: 7 rows per block).  Each row's
+// W partial 16-vectors meet in LDS behind a bare s_barrier (no vmcnt drain: the next rows' tiles
+// stay in flight) and one wave applies the epilogue.  Row r's output is sum_w (MFMA chain of
+// wave w over its k-tiles), the W partials added in a fixed tree order: deterministic.
+//
+// RMSNorm (nrm): each wave sums the squares of its own x words (the waves cover the row once), the
+// W sums meet in LDS (bare s_barrier, fixed order), and every x word is normalised as the
+// reference rounds it — x_hat = RN16(weight * (x * rsqrt(mean(x^2) + eps))), fp32 inside — before
+// it is parked: the linear then multiplies exactly the reference's normed fp16 row (up to the
+// fp32 ulp of the statistics' summation order).  The norm runs once per block, not per row.
+//
+// Every global load is unconditional (clamped indices) except the last round's refills, so the
+// compiler counts them with vmcnt(N): x words first, then the first PF tiles' codes and
+// (scale, zero) words; the x wait does not wait for the weights.
 // ---------------------------------------------------------------------------------------------
-#ifndef GEMV_NRM_XFIRST  // dev switch: the fused norm's x words issued before the codes
-#define GEMV_NRM_XFIRST 1
+#ifndef GEMV_ROWS_BPC  // dev knob: resident blocks per CU of a persistent (multi-row) launch
+#define GEMV_ROWS_BPC 1
 #endif
-#ifndef GEMV_NRM_LATE  // 1 (round 3): the norm's rsqrt is applied to the accumulators in the
-#define GEMV_NRM_LATE 1  // epilogue (x words rounded as RN16(w * x)): the first MFMAs wait for no
-#endif                   // statistics; 0: the round-2 form (statistics behind a barrier first)
-// qlin_rmsnorm_linear_ep_f16's optional inputs (precomputed statistics, RoPE row gather)
-struct NormIn {
-  const float* sq_in;
-  int sq_n;
-  const int64_t* rope_pos;
-  const float* rope_cos;
-  const float* rope_sin;
-  int64_t rope_rows;
-  float* rope_out;
+#ifndef GEMV_ROWS_CONTIG  // dev knob: 1 = wave w takes k-tiles w*TPW .. (w+1)*TPW - 1,
+#define GEMV_ROWS_CONTIG 0  // 0 = k-tiles w, w + W, w + 2W, ... (same arithmetic, other addresses)
+#endif
+#ifndef GEMV_ROWS_MAXPF  // dev knob: most tiles in flight per wave
+#define GEMV_ROWS_MAXPF 8
+#endif
+constexpr int kRowsMaxTPW = 8;  // k-tiles per wave and row: x words held in registers at start
+
+struct RowsArgs {
+  const uint32_t* qw;   // tile row 0 of qweight
+  const uint32_t* qsz;  // tile row 0 of qsz
+  const _Float16* x;
+  const _Float16* bias;
+  const _Float16* res;  // kEpResidual
+  _Float16* y;
+  const float* nw;      // nrm: RMSNorm weight, fp32 [K]
+  float eps;
+  int ep, nrm;
+  int N, K, Kt, G, Nt;
+  int W, TPW;           // waves per block, k-tiles per wave and row (W * TPW == Kt)
+  int nb;               // blocks of the grid: block b owns tile rows b, b + nb, ...
+  int kt0m, kts;        // wave w's k-tile i = w * kt0m + i * kts
+  uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
 };
 
+template <int BITS, int GPT, int ZM, int PF>
+__global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t xs_dyn[];  // [W][TPW][64] x words
+  __shared__ __attribute__((aligned(16))) float red[2][kTileN][kMaxWaves];  // row partials
+  __shared__ float nss[kMaxWaves];                                          // nrm: sums of squares
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, n_in = lane & 15;
+  const int b = blockIdx.x;
+  const int TPW = a.TPW;
+  const int nrows = (a.Nt - 1 - b) / a.nb + 1;  // >= 1
+  const int T = nrows * TPW;                    // tiles this wave streams (host: T >= PF)
+  const int kt0 = wave * a.kt0m;
+  uint32_t* xsl = xs_dyn + wave * TPW * 64;
+  const int64_t wrow = (int64_t)a.Kt * (64 * BITS);  // qweight words per tile row
+  const int64_t srow = (int64_t)a.G * kTileN;          // qsz words per tile row
+  auto group_of_tile = [&](int kt) {
+    return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
+  };
+
+  // x words of this wave's k-tiles (lane l: k = 128 kt + 2l, 2l + 1), the same for every row;
+  // slots past TPW repeat the last tile (L1 hits, never used)
+  uint32_t xw[kRowsMaxTPW];
+  float2 nwv[kRowsMaxTPW];
+#pragma unroll
+  for (int i = 0; i < kRowsMaxTPW; ++i) {
+    const int kt = kt0 + min(i, TPW - 1) * a.kts;
+    xw[i] = *reinterpret_cast<const uint32_t*>(a.x + kt * kTileK + 2 * lane);
+  }
+  if (a.nrm) {  // block-uniform
+#pragma unroll
+    for (int i = 0; i < kRowsMaxTPW; ++i) {
+      const int kt = kt0 + min(i, TPW - 1) * a.kts;
+      nwv[i] = *reinterpret_cast<const float2*>(a.nw + kt * kTileK + 2 * lane);
+    }
+  }
+
+  // weight stream: the load cursor (row jl, k-tile il) runs PF tiles ahead of the compute cursor
+  WTile<BITS, GPT> wt[PF];
+  int il = 0;
+  int64_t lq = (int64_t)b * wrow, ls = (int64_t)b * srow;  // the load row's qweight / qsz offsets
+  auto load = [&](int u) {
+    const int kt = kt0 + il * a.kts;
+    wt[u].pc = load_piece_nt<BITS>(a.qw + lq + kt * (64 * BITS) + lane * BITS);
+    const int g0 = group_of_tile(kt);
+#pragma unroll
+    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = a.qsz[ls + (g0 + s) * kTileN + n_in];
+    if (++il == TPW) {
+      il = 0;
+      lq += (int64_t)a.nb * wrow;
+      ls += (int64_t)a.nb * srow;
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load(u);
+
+  // the epilogue operands of the first row this wave finishes (row j = wave: the epilogue of row j
+  // runs on wave j % W), fetched while the weights stream
+  const int NO = a.ep == kEpSiluMul ? 8 : kTileN;  // outputs per row
+  const int on = min(lane, NO - 1);
+  _Float16 ob0 = 0, ob1 = 0, ores = 0;
+  auto load_epi = [&](int j) {
+    const int64_t row = (int64_t)(b + min(j, nrows - 1) * a.nb) * kTileN + on;
+    const int64_t rc = min(row, (int64_t)a.N - 1);
+    if (a.bias) {
+      ob0 = a.bias[rc];
+      ob1 = a.bias[min(row + 8, (int64_t)a.N - 1)];
+    }
+    if (a.ep == kEpResidual) ores = a.res[rc];
+  };
+  load_epi(wave);
+
+  if (wave == 0 && lane < kTileN) {  // partial columns of absent waves read as zero
+    for (int w = a.W; w < kMaxWaves; ++w) red[0][lane][w] = red[1][lane][w] = 0.f;
+  }
+
+  if (a.nrm) {
+#pragma clang fp contract(off)
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < kRowsMaxTPW; ++i) {
+      if (i < TPW) {
+        const h2 v = as_h2(xw[i]);
+        const float f0 = (float)v.x, f1 = (float)v.y;
+        ss = ss + f0 * f0;
+        ss = ss + f1 * f1;
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) nss[wave] = ss;
+    // a bare s_barrier: __syncthreads() would also wait for the weight tiles in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float tot = 0.f;
+    for (int w = 0; w < a.W; ++w) tot += nss[w];
+    const float rn = rsqrtf(tot / (float)a.K + a.eps);
+#pragma unroll
+    for (int i = 0; i < kRowsMaxTPW; ++i) {
+      const h2 v = as_h2(xw[i]);
+      const float n0 = nwv[i].x * ((float)v.x * rn);
+      const float n1 = nwv[i].y * ((float)v.y * rn);
+      xw[i] = as_u32(h2{(_Float16)n0, (_Float16)n1});
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kRowsMaxTPW; ++i)
+    if (i < TPW) xsl[i * 64 + lane] = xw[i];
+
+  const Magics mg = make_magics<BITS>();
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  int ic = 0, jc = 0, ew = 0, par = 0;  // compute cursor, epilogue wave, partial buffer
+  auto epilogue = [&]() {
+    if (lane < kTileN) red[par][lane][wave] = acc[0];
+    acc = f4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (wave == ew) {  // wave-uniform
+      const int64_t r = (int64_t)b + (int64_t)jc * a.nb;
+      auto total = [&](int n, _Float16 bv) {
+        const f4* p = reinterpret_cast<const f4*>(&red[par][n][0]);
+        const f4 e = (p[0] + p[1]) + (p[2] + p[3]);
+        float t = (e[0] + e[1]) + (e[2] + e[3]);
+        if (a.bias) t += (float)bv;
+        return (float)(_Float16)t;  // F.linear's fp16 output
+      };
+      if (lane < NO) {
+        if (a.ep == kEpSiluMul) {
+          if (r * kTileN + lane + 8 < a.N)
+            a.y[r * 8 + lane] = (_Float16)(silu_rn16(total(lane, ob0)) * total(lane + 8, ob1));
+        } else if (r * kTileN + lane < a.N) {
+          float t = total(lane, ob0);
+          if (a.ep == kEpResidual) t += (float)ores;
+          a.y[r * kTileN + lane] = (_Float16)t;
+        }
+      }
+      load_epi(jc + a.W);  // this wave's next epilogue row
+    }
+    if (++ew == a.W) ew = 0;
+    par ^= 1;
+  };
+  auto compute = [&](int u) {
+    const uint4* xb = reinterpret_cast<const uint4*>(xsl + ic * 64) + (lane >> 4);
+    h8 xa[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, xb[4 * s]);
+    auto step = [&](auto S_) {
+      constexpr int S = decltype(S_)::value;
+      uint32_t v[4];
+      const GroupQ gq = make_group_w<BITS, ZM>(wt[u].sz[S * GPT / 4]);
+      dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
+      const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    if (++ic == TPW) {  // block-uniform: the row is complete in every wave
+      epilogue();
+      ic = 0;
+      ++jc;
+    }
+  };
+
+  // rounds of PF tiles; every refill of all but the last full round is in range
+  const int Q = T / PF;  // >= 1
+  for (int q = 0; q + 1 < Q; ++q) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      compute(u);
+      load(u);
+    }
+  }
+  const int rem = T - Q * PF;  // tiles after the last full round (< PF)
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    compute(u);
+    if (u < rem) load(u);
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < rem) compute(u);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode fast path for 2..4 token rows: M <= 4, K % 128 == 0, group % 128 == 0 or group in
+// {32, 64}, no activation fake-quant.  Same arithmetic as gemv_kernel (exact W_dq, one MFMA per
+// k-step), built for the few microseconds a decode launch lasts (tools/dev/gemv_lab2.hip,
+// gemv_lab3.hip): block = one tile row, W waves split K (k-tiles w, w + W, ...),
+// every size-derived value precomputed on the host, all of a wave's tiles loaded up front.
+// ---------------------------------------------------------------------------------------------
 struct FastArgs {
   const uint32_t* qw;   // row tile 0 of qweight
   const uint32_t* qsz;  // row tile 0 of qsz
@@ -394,191 +592,62 @@ struct FastArgs {
   int M, N, K, Kt, G;
   int W, lw;            // waves per block (power of two), log2 W
   uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
-  const float* nw;      // NRM: RMSNorm weight (fp32 [K]) applied to x first
-  float eps;
-  const float* sq_in;   // NRM: precomputed statistics (sq_n partial sums of squares of x), or null
-  int sq_n;
-  float* sq_out;        // EP == kEpResidual, M == 1: per-tile sums of squares of y, or null
-  const int64_t* rope_pos;  // block 0, wave 0: copy cos / sin row rope_pos[0] to rope_out
-  const float* rope_cos;
-  const float* rope_sin;
-  int64_t rope_rows;
-  float* rope_out;      // [2][128] fp32, or null
 };
-constexpr int kSqMaxPerLane = 8;  // sumsq_in partials per lane (K <= 64 * 8 * 16 = 8192)
 
-// every wave streams at most PF tiles, all of them loaded up front (no refill loop: a launch whose
-// waves need more tiles takes gemv_kernel, whose contiguous tile runs stream better then).
-// NRM (M = 1): x is the decoder layer's hidden state before its RMSNorm (OmniLlamaRMSNorm,
-// quant/omni_norm.py:52-63 of the reference) and the kernel applies the norm itself: each wave
-// sums the squares of the x words it loads anyway (its own tiles; together the waves cover the
-// row once), the block combines the W wave sums through LDS behind a bare s_barrier (no vmcnt
-// drain), and every x word is normalised (weight * (x * rsqrt(mean + eps)), fp32, rounded to fp16
-// as the norm's output) before it is parked.  One launch instead of two (the separate
-// qlin_rmsnorm_f16); the sum of squares runs in another order than that kernel's, so the normed
-// x can differ from it by an fp16 ulp.
-template <int BITS, int MT, int GPT, int ZM, int EP, int PF, bool NRM = false>
+template <int BITS, int MT, int GPT, int ZM, int EP, int PF>
 __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
-  __shared__ float nss[NRM ? kMaxWaves : 1];  // NRM: per-wave sums of squares
-  static_assert(!NRM || MT == 1, "the fused RMSNorm serves one token row");
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
   const int nt = blockIdx.x;
-  const _Float16* ax = a.x;
-  const _Float16* abias = a.bias;
-  _Float16* ay = a.y;
   const uint32_t* qw = a.qw + (int64_t)nt * a.Kt * (64 * BITS) + lane * BITS;
   const uint32_t* sz = a.qsz + (int64_t)nt * a.G * kTileN + n_in;
   constexpr int LPR = 64 / MT;  // lanes per x row
-  const _Float16* xr = ax + (int64_t)min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
+  const _Float16* xr = a.x + (int64_t)min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
   const int nts = (a.Kt - wave + a.W - 1) >> a.lw;  // >= 1: W <= Kt
   const int ktl = wave + ((nts - 1) << a.lw);        // the wave's last tile
-
-  // precomputed norm statistics: issued before every other load (in-order completion: the norm
-  // then waits for these alone, not for the weights)
-  float sqp[NRM ? kSqMaxPerLane : 1];
-  if constexpr (NRM && !GEMV_NRM_LATE) {
-    if (a.sq_in) {
-#pragma unroll
-      for (int i = 0; i < kSqMaxPerLane; ++i) sqp[i] = a.sq_in[min(lane + 64 * i, a.sq_n - 1)];
-    }
-  }
-  if (a.rope_out && nt == 0 && wave == 0) {
-    // the step's RoPE cos / sin row for the attention launch that follows (it then skips the
-    // position -> row round trip); tiny, and only block 0's wave 0 pays it
-    const int64_t p = min(max(a.rope_pos[0], (int64_t)0), a.rope_rows - 1);
-    const float* src = (lane < 32 ? a.rope_cos : a.rope_sin) + p * 128 + 4 * (lane & 31);
-    *reinterpret_cast<float4*>(a.rope_out + 4 * lane) = *reinterpret_cast<const float4*>(src);
-  }
   auto kt_of = [&](int i) { return min(wave + (i << a.lw), ktl); };
   auto group_of_tile = [&](int kt) {
     return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
   };
   WTile<BITS, GPT> wt[PF];
   XRaw<MT> xq[PF];
-  float2 nwv[NRM ? PF : 1];  // NRM: norm weights of the lane's two x halves per tile
-  auto load_codes = [&](int u, int kt) { wt[u].pc = load_piece_nt<BITS>(qw + kt * (64 * BITS)); };
-  auto load_sz = [&](int u, int kt) {
+#pragma unroll
+  for (int u = 0; u < PF; ++u) wt[u].pc = load_piece_nt<BITS>(qw + kt_of(u) * (64 * BITS));
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const int kt = kt_of(u);
     const int g0 = group_of_tile(kt);
 #pragma unroll
     for (int s = 0; s < GPT; ++s) wt[u].sz[s] = sz[(g0 + s) * kTileN];
-  };
-  auto load_x = [&](int u, int kt) {
     const _Float16* p = xr + kt * kTileK;
-    if constexpr (MT == 1) {
-      xq[u].w[0] = *reinterpret_cast<const uint32_t*>(p);
-    } else if constexpr (MT == 2) {
+    if constexpr (MT == 2) {
       const uint2 v = *reinterpret_cast<const uint2*>(p);
       xq[u].w[0] = v.x; xq[u].w[1] = v.y;
     } else {
       const uint4 v = *reinterpret_cast<const uint4*>(p);
       xq[u].w[0] = v.x; xq[u].w[1] = v.y; xq[u].w[2] = v.z; xq[u].w[3] = v.w;
     }
-  };
-  if constexpr (NRM) {
-#if GEMV_NRM_XFIRST
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      load_x(u, kt_of(u));
-      nwv[u] = *reinterpret_cast<const float2*>(a.nw + kt_of(u) * kTileK + 2 * lane);
-    }
-#pragma unroll
-    for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
-#else
-#pragma unroll
-    for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      load_x(u, kt_of(u));
-      nwv[u] = *reinterpret_cast<const float2*>(a.nw + kt_of(u) * kTileK + 2 * lane);
-    }
-#endif
-#pragma unroll
-    for (int u = 0; u < PF; ++u) load_sz(u, kt_of(u));
-  } else {
-#pragma unroll
-    for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      load_sz(u, kt_of(u));
-      load_x(u, kt_of(u));
-    }
   }
-  // the epilogue's bias / residual operands, fetched while the weights stream (fetched after the
-  // reduction they would cost one more round trip).  Only wave 0's lanes use them, but every wave
-  // loads (clamped, L2-resident): a load under a branch is waited for at the branch's join
+  // the epilogue's bias / residual operands, fetched while the weights stream (every wave loads,
+  // clamped: a load under a branch is waited for at the branch's join)
   constexpr int NO = EP == kEpSiluMul ? MT * 8 : MT * kTileN;  // outputs per block
-  const int om = min(tid / (NO / MT), a.M - 1), on = tid % (NO / MT);  // output (row m, column n)
+  const int om = min(tid / (NO / MT), a.M - 1), on = tid % (NO / MT);
   const int64_t orow = (int64_t)nt * kTileN + on;
   const bool oval = tid < NO && tid / (NO / MT) < a.M && orow + (EP == kEpSiluMul ? 8 : 0) < a.N;
-  const _Float16* bsrc = abias ? abias + min(orow, (int64_t)a.N - 1) : ax;
+  const _Float16* bsrc = a.bias ? a.bias + min(orow, (int64_t)a.N - 1) : a.x;
   const _Float16 ob0 = bsrc[0];
-  const _Float16 ob1 = EP == kEpSiluMul ? bsrc[abias ? 8 : 0] : ob0;
+  const _Float16 ob1 = EP == kEpSiluMul ? bsrc[a.bias ? 8 : 0] : ob0;
   _Float16 ores = 0;
   if constexpr (EP == kEpResidual) ores = a.res[(int64_t)om * a.N + min(orow, (int64_t)a.N - 1)];
-
-  float rn = 1.f;  // NRM: rsqrt(mean(x^2) + eps)
-  float ss_late = 0.f;  // GEMV_NRM_LATE: this wave's sum of squares of its x words
-  if constexpr (NRM && GEMV_NRM_LATE) {
-#pragma clang fp contract(off)
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      if (u < nts) {
-        const h2 v = as_h2(xq[u].w[0]);
-        const float f0 = (float)v.x, f1 = (float)v.y;
-        ss_late = ss_late + f0 * f0;
-        ss_late = ss_late + f1 * f1;
-      }
-    }
-  } else if constexpr (NRM) {
-   if (a.sq_in) {
-#pragma clang fp contract(off)
-    // sum of partial i over i = lane + 64 j (j in order), then the wave butterfly: the same
-    // order in every wave and block, and no barrier
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < kSqMaxPerLane; ++i)
-      if (lane + 64 * i < a.sq_n) ss = ss + sqp[i];
-    ss = wave_sum(ss);
-    rn = rsqrtf(ss / (float)a.K + a.eps);
-   } else {
-#pragma clang fp contract(off)
-    float ss = 0.f;
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      if (u < nts) {  // wave-uniform: slots past the wave's tiles repeat its last tile
-        const h2 v = as_h2(xq[u].w[0]);
-        const float f0 = (float)v.x, f1 = (float)v.y;
-        ss = ss + f0 * f0;
-        ss = ss + f1 * f1;
-      }
-    }
-    ss = wave_sum(ss);
-    if (lane == 0) nss[wave] = ss;
-    // a bare s_barrier after the LDS store: __syncthreads() would also drain vmcnt, i.e. wait for
-    // the sz words still in flight; the waves only need each other's sums
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    float tot = 0.f;
-    for (int w = 0; w < a.W; ++w) tot += nss[w];
-    rn = rsqrtf(tot / (float)a.K + a.eps);
-   }
-  }
 
   const Magics mg = make_magics<BITS>();
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   uint32_t* slot = &xs[wave][0];
   auto tile = [&](int u) {
     h8 xa[4];
-    if constexpr (NRM) {
-#pragma clang fp contract(off)
-      const h2 v = as_h2(xq[u].w[0]);
-      const float n0 = GEMV_NRM_LATE ? nwv[u].x * (float)v.x : nwv[u].x * ((float)v.x * rn);
-      const float n1 = GEMV_NRM_LATE ? nwv[u].y * (float)v.y : nwv[u].y * ((float)v.y * rn);
-      xq[u].w[0] = as_u32(h2{(_Float16)n0, (_Float16)n1});
-    }
     park_x<MT>(xa, xq[u], slot, lane, n_in);
     auto step = [&](auto S_) {
       constexpr int S = decltype(S_)::value;
@@ -594,9 +663,7 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
     step(std::integral_constant<int, 3>{});
   };
   // every slot is computed — a slot past the wave's tiles (a repeat of its last tile) with x
-  // zeroed — so the compiler cannot sink those slots' loads behind a branch (which it does for
-  // `if (u < nts) tile(u)`: the loads then issue only after the earlier tiles' compute, one
-  // extra HBM round trip per launch)
+  // zeroed — so the compiler cannot sink those slots' loads behind a branch
   tile(0);  // nts >= 1
 #pragma unroll
   for (int u = 1; u < PF; ++u) {
@@ -617,47 +684,24 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
 #pragma unroll
         for (int e = 0; e < 4 && e < MT; ++e) red[((q4 + e) * kTileN + n_in) * kMaxWaves + w] = 0.f;
   }
-  if constexpr (NRM && GEMV_NRM_LATE) {
-    const float ssw = wave_sum(ss_late);
-    if (lane == 0) nss[wave] = ssw;
-  }
   __syncthreads();
-  if constexpr (NRM && GEMV_NRM_LATE) {
-    if (wave == 0) {  // the outputs are formed by wave 0
-#pragma clang fp contract(off)
-      float tot = 0.f;
-      if (a.sq_in) {  // precomputed statistics (fixed order: every block forms the same value)
-        for (int i = 0; i < a.sq_n; ++i) tot += a.sq_in[i];
-      } else {
-        for (int w = 0; w < a.W; ++w) tot += nss[w];
-      }
-      rn = rsqrtf(tot / (float)a.K + a.eps);
-    }
-  }
   auto total = [&](int o, _Float16 b) {
     const f4* r = reinterpret_cast<const f4*>(red + o * kMaxWaves);
     const f4 p = r[0], q = r[1], c = r[2], d = r[3];
     const f4 e = (p + q) + (c + d);
     float t = (e[0] + e[1]) + (e[2] + e[3]);
-    if (NRM && GEMV_NRM_LATE) t = t * rn;
-    if (abias) t += (float)b;
+    if (a.bias) t += (float)b;
     return (float)(_Float16)t;  // F.linear's fp16 output
   };
-  float sqv = 0.f;  // sq_out: this thread's output squared
   if (oval) {  // wave 0 only (tid < NO <= 64)
     if constexpr (EP == kEpSiluMul) {  // 8 outputs per tile and row
       const float g = total(om * kTileN + on, ob0), u = total(om * kTileN + on + 8, ob1);
-      ay[(int64_t)om * (a.N >> 1) + nt * 8 + on] = (_Float16)(silu_rn16(g) * u);
+      a.y[(int64_t)om * (a.N >> 1) + nt * 8 + on] = (_Float16)(silu_rn16(g) * u);
     } else {
       float t = total(om * kTileN + on, ob0);
       if constexpr (EP == kEpResidual) t += (float)ores;
-      ay[(int64_t)om * a.N + orow] = (_Float16)t;
-      const float f = (float)(_Float16)t;
-      sqv = f * f;
+      a.y[(int64_t)om * a.N + orow] = (_Float16)t;
     }
-  }
-  if constexpr (EP == kEpResidual && MT == 1) {
-    if (a.sq_out && wave == 0) sq_tile_out(sqv, a.sq_out, nt);
   }
 }
 
@@ -695,9 +739,14 @@ __global__ __launch_bounds__(256) void dequant_kernel(
   one(std::integral_constant<int, 3>{});
 }
 
-uint32_t group_magic(int group) {
+inline uint32_t group_magic(int group) {
   const uint64_t d = (uint64_t)(group / 32);
   return (uint32_t)(((1ull << 31) + d - 1) / d);
+}
+
+inline uint32_t tile_group_magic(int group) {  // GPT == 1: kt / (group / 128) = (kt * magic) >> 31
+  const uint64_t c = group % kTileK == 0 ? (uint64_t)(group / kTileK) : 1;
+  return (uint32_t)(((1ull << 31) + c - 1) / c);
 }
 
 // waves per block: grow W until the grid holds ~32 waves for each of the 256 CUs; on grids of
@@ -707,7 +756,7 @@ uint32_t group_magic(int group) {
 #ifndef GEMV_WAVE_TARGET  // dev sweep knob (tools/dev/Makefile libgv*.so)
 #define GEMV_WAVE_TARGET 8192
 #endif
-int pick_waves(int Nt, int Kt, int& tpw) {
+inline int pick_waves(int Nt, int Kt, int& tpw) {
   int W = 1;
   while (W < kMaxWaves && (int64_t)Nt * W < GEMV_WAVE_TARGET && (Nt < 512 || Kt >= 8 * W)) W *= 2;
   W = min(W, Kt);
@@ -731,8 +780,7 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
 #define QLIN_GV(PF, T)                                                                     \
   hipLaunchKernelGGL((gemv_kernel<BITS, MT, GPT, ZM, PF, T>), dim3(blocks), dim3(64 * W), \
                      0, st, qw, qsz, (const _Float16*)x, (const _Float16*)bias,             \
-                     (_Float16*)y, M, N, K, group, gs, tpw, (const _Float16*)e.res, e.ep, e.aq,   \
-                     e.sq_out)
+                     (_Float16*)y, M, N, K, group, gs, tpw, (const _Float16*)e.res, e.ep, e.aq)
   if constexpr (MT >= 8) {  // x registers of 4 tiles in flight would spill
     if (ntb == 2) QLIN_GV(2, 2);
     else QLIN_GV(2, 1);
@@ -747,65 +795,123 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   return (int)hipGetLastError();
 }
 
-// the decode fast path (gemv_fast_kernel): M <= 4, K % 128 == 0, whole or 32 / 64-wide groups
-bool fast_ok(int M, int K, int group, const Ep& e) {
-  return M <= 4 && K % kTileK == 0 && !e.aq.on &&
-         (group % kTileK == 0 || group == 32 || group == 64);
+inline bool group_fast(int K, int group) {  // whole-tile or 32 / 64-wide groups on whole k-tiles
+  return K % kTileK == 0 && (group % kTileK == 0 || group == 32 || group == 64);
+}
+
+// ---- M == 1: the rows kernel ------------------------------------------------------------------
+struct RowsGeo {
+  int W, TPW, nb, pf;
+};
+
+// W * TPW == Kt with TPW the smallest of {2, 4, 8} that keeps W <= 16 (the most waves per row);
+// one row per block up to 2 rows per CU, else a persistent grid of GEMV_ROWS_BPC blocks per CU;
+// PF = the wave's whole row (one-row blocks) or 4 / 8 tiles across rows
+#ifndef GEMV_ROWS_MINTPW  // dev knob: smallest k-tiles per wave and row
+#define GEMV_ROWS_MINTPW 2
+#endif
+inline bool rows_geometry(int64_t Nt, int Kt, RowsGeo& g) {
+  g.TPW = 0;
+  for (int t = GEMV_ROWS_MINTPW; t <= kRowsMaxTPW; t *= 2)
+    if (Kt % t == 0 && Kt / t <= kMaxWaves) {
+      g.TPW = t;
+      break;
+    }
+  if (!g.TPW || Nt < 1 || Nt > (1 << 26)) return false;
+  g.W = Kt / g.TPW;
+  const int64_t cus = device_cu_count();
+  g.nb = Nt <= 2 * cus ? (int)Nt : (int)(cus * GEMV_ROWS_BPC);
+  const int64_t tmin = (Nt / g.nb) * g.TPW;  // fewest tiles any wave streams
+  g.pf = 2;
+  while (g.pf * 2 <= GEMV_ROWS_MAXPF && g.pf * 2 <= tmin) g.pf *= 2;
+  return true;
+}
+
+inline bool rows_ok(int M, int K, int group, const Ep& e) {
+  RowsGeo g;
+  return M == 1 && !e.aq.on && group_fast(K, group) && rows_geometry(1, K / kTileK, g);
+}
+
+template <int BITS, int GPT, int ZM>
+int launch_rows(RowsArgs a, const RowsGeo& g, hipStream_t st) {
+  a.W = g.W;
+  a.TPW = g.TPW;
+  a.nb = g.nb;
+  a.kt0m = GEMV_ROWS_CONTIG ? g.TPW : 1;
+  a.kts = GEMV_ROWS_CONTIG ? 1 : g.W;
+  const size_t lds = (size_t)g.W * g.TPW * 64 * sizeof(uint32_t);
+#define QLIN_GR(PF)                                                                             \
+  hipLaunchKernelGGL((gemv_rows_kernel<BITS, GPT, ZM, PF>), dim3((unsigned)g.nb), dim3(64 * g.W), \
+                     lds, st, a)
+  if (g.pf >= 8) QLIN_GR(8);
+  else if (g.pf == 4) QLIN_GR(4);
+  else QLIN_GR(2);
+#undef QLIN_GR
+  return (int)hipGetLastError();
+}
+
+template <int BITS, int ZM>
+int launch_rows_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
+                  uint16_t* y, int N, int K, int group, hipStream_t st, int ep,
+                  const uint16_t* res, const float* nw, float eps) {
+  RowsGeo g;
+  const int64_t Nt = (N + kTileN - 1) / kTileN;
+  if (!rows_geometry(Nt, K / kTileK, g)) return QLIN_EINVAL;
+  RowsArgs a;
+  a.qw = qw;
+  a.qsz = qsz;
+  a.x = (const _Float16*)x;
+  a.bias = (const _Float16*)bias;
+  a.res = (const _Float16*)res;
+  a.y = (_Float16*)y;
+  a.nw = nw;
+  a.eps = eps;
+  a.ep = ep;
+  a.nrm = nw != nullptr;
+  a.N = N;
+  a.K = K;
+  a.Kt = K / kTileK;
+  a.G = K / group;
+  a.Nt = (int)Nt;
+  a.cmagic = tile_group_magic(group);
+  if (group % kTileK == 0) return launch_rows<BITS, 1, ZM>(a, g, st);
+  if (group == 64) return launch_rows<BITS, 2, ZM>(a, g, st);
+  return launch_rows<BITS, 4, ZM>(a, g, st);
+}
+
+// ---- M == 2..4: the fast kernel --------------------------------------------------------------
+inline bool fast_ok(int M, int K, int group, const Ep& e) {
+  return M >= 2 && M <= 4 && !e.aq.on && group_fast(K, group);
 }
 
 template <int BITS, int MT, int GPT, int ZM, int EP>
 int launch_fast_t(const FastArgs& a, int Nt, int tpw, hipStream_t st) {
-#define QLIN_GF(PF, NR)                                                                      \
-  hipLaunchKernelGGL((gemv_fast_kernel<BITS, MT, GPT, ZM, EP, PF, NR>), dim3(Nt),          \
-                     dim3(64 * a.W), 0, st, a)
-  if constexpr (MT == 1) {
-    if (a.nw) {
-      if (tpw <= 2) QLIN_GF(2, true);
-      else if (tpw <= 4) QLIN_GF(4, true);
-      else QLIN_GF(8, true);
-      return (int)hipGetLastError();
-    }
-  }
-  if (tpw <= 2) QLIN_GF(2, false);
-  else if (tpw <= 4) QLIN_GF(4, false);
-  else QLIN_GF(8, false);
+#define QLIN_GF(PF)                                                                          \
+  hipLaunchKernelGGL((gemv_fast_kernel<BITS, MT, GPT, ZM, EP, PF>), dim3(Nt), dim3(64 * a.W), \
+                     0, st, a)
+  if (tpw <= 2) QLIN_GF(2);
+  else QLIN_GF(4);
 #undef QLIN_GF
   return (int)hipGetLastError();
 }
 
 // fast-path geometry: pick_waves rounded down to a power of two; the fast path takes launches
-// whose waves stream at most 4 tiles (tools/dev/fast_geo.py, M = 1: 4096 x 4096 W = 16 x 2 tiles
-// 4.30 -> 3.76 us, 6144 x 4096 5.48 -> 5.02, 28672 x 4096 W = 8 x 4 13.55 -> 12.67; the
-// LLaMA down projection 4096 x 14336, 7 tiles per wave, stays on gemv_kernel: 7.8 vs 8.3 us)
-#ifndef GEMV_FAST_MAX_TPW  // dev sweep knob: tiles per wave the fast path takes (4 or 8)
-#define GEMV_FAST_MAX_TPW 4
-#endif
-bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
+// whose waves stream at most 4 tiles (tools/dev/fast_geo.py)
+inline bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
   W = pick_waves(Nt, Kt, tpw);
   lw = 0;
   while ((2 << lw) <= W) ++lw;  // round W down to a power of two (W <= Kt)
   W = 1 << lw;
   tpw = (Kt + W - 1) / W;
-  return tpw <= GEMV_FAST_MAX_TPW;
+  return tpw <= 4;
 }
 
 template <int BITS, int MT, int ZM>
 int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                 uint16_t* y, int M, int N, int K, int group, int W, int lw, int tpw,
-                hipStream_t st, const Ep& e, const float* nw = nullptr, float eps = 0.f,
-                const NormIn* ni = nullptr) {
+                hipStream_t st, const Ep& e) {
   const int Nt = (N + kTileN - 1) / kTileN;
   FastArgs a;
-  a.nw = nw;
-  a.eps = eps;
-  a.sq_out = e.sq_out;
-  a.sq_in = ni ? ni->sq_in : nullptr;
-  a.sq_n = ni ? ni->sq_n : 0;
-  a.rope_pos = ni ? ni->rope_pos : nullptr;
-  a.rope_cos = ni ? ni->rope_cos : nullptr;
-  a.rope_sin = ni ? ni->rope_sin : nullptr;
-  a.rope_rows = ni ? ni->rope_rows : 0;
-  a.rope_out = ni ? ni->rope_out : nullptr;
   a.qw = qw;
   a.qsz = qsz;
   a.x = (const _Float16*)x;
@@ -819,8 +925,7 @@ int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   a.G = K / group;
   a.W = W;
   a.lw = lw;
-  const uint64_t c = group % kTileK == 0 ? (uint64_t)(group / kTileK) : 1;
-  a.cmagic = (uint32_t)(((1ull << 31) + c - 1) / c);
+  a.cmagic = tile_group_magic(group);
 #define QLIN_FE(GPT)                                                                           \
   return e.ep == kEpResidual  ? launch_fast_t<BITS, MT, GPT, ZM, kEpResidual>(a, Nt, tpw, st)  \
          : e.ep == kEpSiluMul ? launch_fast_t<BITS, MT, GPT, ZM, kEpSiluMul>(a, Nt, tpw, st)   \
@@ -844,15 +949,14 @@ int launch_gemv_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
 template <int BITS, int ZM>
 int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st, const Ep& e) {
+  if (rows_ok(M, K, group, e))
+    return launch_rows_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, e.ep, e.res, nullptr,
+                                   0.f);
   int W = 0, lw = 0, tpw = 0;
   if (fast_ok(M, K, group, e) &&
       fast_geometry((N + kTileN - 1) / kTileN, K / kTileK, W, lw, tpw)) {
-#define QLIN_F(MT) \
-  return launch_fast<BITS, MT, ZM>(qw, qsz, x, bias, y, M, N, K, group, W, lw, tpw, st, e)
-    if (M == 1) QLIN_F(1);
-    if (M == 2) QLIN_F(2);
-    QLIN_F(4);
-#undef QLIN_F
+    if (M == 2) return launch_fast<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, W, lw, tpw, st, e);
+    return launch_fast<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, W, lw, tpw, st, e);
   }
   if (M == 1) return launch_gemv_g<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   if (M == 2) return launch_gemv_g<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
@@ -861,7 +965,32 @@ int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   return launch_gemv_g<BITS, 16, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
 }
 
-}  // namespace
+}  // namespace qlin_gv
+
+// The kernel instances of each bit width are compiled in a translation unit of their own (the
+// Makefile builds this file once per width with -DQLIN_GEMV_BITS=b, and once without it for the
+// entry points), so they compile in parallel.
+#define QLIN_GV_INST(EXT, B, Z)                                                                  \
+  EXT template int qlin_gv::launch_gemv_m<B, Z>(const uint32_t*, const uint32_t*, const uint16_t*, \
+                                                const uint16_t*, uint16_t*, int, int, int, int,    \
+                                                hipStream_t, const qlin_gv::Ep&);                \
+  EXT template int qlin_gv::launch_rows_g<B, Z>(const uint32_t*, const uint32_t*, const uint16_t*, \
+                                                const uint16_t*, uint16_t*, int, int, int,         \
+                                                hipStream_t, int, const uint16_t*, const float*,   \
+                                                float)
+#define QLIN_GV_INST_B(EXT, B)           \
+  QLIN_GV_INST(EXT, B, kZNarrow);        \
+  QLIN_GV_INST(EXT, B, kZWide);          \
+  QLIN_GV_INST(EXT, B, kZFloat)
+#ifdef QLIN_GEMV_BITS
+QLIN_GV_INST_B(, QLIN_GEMV_BITS);
+#else
+QLIN_GV_INST_B(extern, 2);
+QLIN_GV_INST_B(extern, 3);
+QLIN_GV_INST_B(extern, 4);
+QLIN_GV_INST_B(extern, 8);
+
+using namespace qlin_gv;
 
 extern "C" int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, int64_t N,
                                 int64_t K, int bits, int group, uint16_t* w, void* stream) {
@@ -894,10 +1023,9 @@ extern "C" int qlin_dequant_f16(const uint32_t* qweight, const uint32_t* qsz, in
 int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                   const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t M,
                   int64_t N, int64_t K, int bits, int group, int epilogue, int act_bits,
-                  int act_flags, void* stream, float* sq_out) {
+                  int act_flags, void* stream) {
   if (!qweight || !qsz || !x || !y || M < 1 || M > kGemvMaxM || !valid_layout(N, K, bits, group))
     return QLIN_EINVAL;
-  if (sq_out && (M != 1 || epilogue != kEpResidual)) return QLIN_EINVAL;
   if (act_bits && (act_bits < 2 || act_bits > 8 || K % 8 || ((uintptr_t)x & 15))) return QLIN_EINVAL;
   if (N == 0) return QLIN_OK;
   ActQ aq{act_bits != 0, act_bits, act_flags, 0.f, 0.f};
@@ -906,7 +1034,7 @@ int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const
     aq.qmin = has_zp ? 0.f : -(float)(1 << (act_bits - 1));
     aq.qmax = has_zp ? (float)((1 << act_bits) - 1) : (float)((1 << (act_bits - 1)) - 1);
   }
-  const Ep e{residual, epilogue, aq, sq_out};
+  const Ep e{residual, epilogue, aq};
   hipStream_t st = (hipStream_t)stream;
   const int m = (int)M, n = (int)N, k = (int)K;
   const int zm = zero_mode(flags);
@@ -923,15 +1051,13 @@ int qlin::gemv_ep(const uint32_t* qweight, const uint32_t* qsz, int flags, const
 #undef QLIN_G
 }
 
-namespace {
-// the fused RMSNorm + linear serves one token row on the fast path (M = 1, K % 128 == 0, whole /
-// 32 / 64-wide groups, <= 4 tiles per wave)
+namespace qlin_gv {
+// the fused RMSNorm + linear serves one token row on the rows kernel (M = 1, K % 128 == 0, whole /
+// 32 / 64-wide groups, Kt = W * TPW with W <= 16, TPW in {2, 4, 8})
 bool rmsnorm_linear_ok(int64_t M, int64_t N, int64_t K, int bits, int group) {
   if (M != 1 || N < 1 || !valid_layout(N, K, bits, group)) return false;
   const Ep e{nullptr, kEpNone, ActQ{false, 0, 0, 0.f, 0.f}};
-  int W = 0, lw = 0, tpw = 0;
-  return fast_ok(1, (int)K, group, e) &&
-         fast_geometry((int)((N + kTileN - 1) / kTileN), (int)(K / kTileK), W, lw, tpw);
+  return rows_ok(1, (int)K, group, e);
 }
 }  // namespace
 
@@ -944,38 +1070,22 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
                                           const uint16_t* x, const float* norm_weight, float eps,
                                           const uint16_t* bias, const uint16_t* residual,
                                           uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
-                                          int group, int epilogue, const float* sumsq_in,
-                                          int64_t sumsq_n, const int64_t* rope_pos,
-                                          const float* rope_cos, const float* rope_sin,
-                                          int64_t rope_rows, float* rope_out, void* stream) {
+                                          int group, int epilogue, void* stream) {
   if (!qweight || !qsz || !x || !norm_weight || !y || !rmsnorm_linear_ok(M, N, K, bits, group) ||
       ((uintptr_t)norm_weight & 7) || ((uintptr_t)x & 3) || !(eps >= 0.f) ||
       epilogue < kEpNone || epilogue > kEpSiluMul || (epilogue == kEpResidual && !residual) ||
       (epilogue == kEpSiluMul && N % kTileN))
     return QLIN_EINVAL;
-  // precomputed statistics: one partial per 16 elements of x (the producing launch's tiles)
-  if (sumsq_in && (sumsq_n != (K + kTileN - 1) / kTileN || sumsq_n > 64 * kSqMaxPerLane))
-    return QLIN_EINVAL;
-  if (rope_out && (!rope_pos || !rope_cos || !rope_sin || rope_rows < 1 ||
-                   ((uintptr_t)rope_out & 15) || ((uintptr_t)rope_cos & 15) ||
-                   ((uintptr_t)rope_sin & 15)))
-    return QLIN_EINVAL;
-  const Ep e{residual, epilogue, ActQ{false, 0, 0, 0.f, 0.f}};
-  const NormIn ni{sumsq_in, (int)sumsq_n, rope_pos, rope_cos, rope_sin, rope_rows, rope_out};
   hipStream_t st = (hipStream_t)stream;
   const int n = (int)N, k = (int)K;
-  int W = 0, lw = 0, tpw = 0;
-  fast_geometry((n + kTileN - 1) / kTileN, k / kTileK, W, lw, tpw);
   const int zm = zero_mode(flags);
-#define QLIN_N(B)                                                                             \
-  return zm == kZFloat                                                                        \
-             ? launch_fast<B, 1, kZFloat>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw, tpw, \
-                                          st, e, norm_weight, eps, &ni)                       \
-         : zm == kZWide                                                                       \
-             ? launch_fast<B, 1, kZWide>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw, tpw,  \
-                                         st, e, norm_weight, eps, &ni)                        \
-             : launch_fast<B, 1, kZNarrow>(qweight, qsz, x, bias, y, 1, n, k, group, W, lw,     \
-                                           tpw, st, e, norm_weight, eps, &ni)
+#define QLIN_N(B)                                                                              \
+  return zm == kZFloat ? launch_rows_g<B, kZFloat>(qweight, qsz, x, bias, y, n, k, group, st,  \
+                                                   epilogue, residual, norm_weight, eps)       \
+         : zm == kZWide ? launch_rows_g<B, kZWide>(qweight, qsz, x, bias, y, n, k, group, st,  \
+                                                   epilogue, residual, norm_weight, eps)       \
+                        : launch_rows_g<B, kZNarrow>(qweight, qsz, x, bias, y, n, k, group, st, \
+                                                     epilogue, residual, norm_weight, eps)
   switch (bits) {
     case 2: QLIN_N(2);
     case 3: QLIN_N(3);
@@ -985,19 +1095,10 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
 #undef QLIN_N
 }
 
-extern "C" int qlin_linear_res_sumsq_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
-                                         const uint16_t* x, const uint16_t* bias,
-                                         const uint16_t* residual, uint16_t* y, int64_t N,
-                                         int64_t K, int bits, int group, float* sumsq_out,
-                                         void* stream) {
-  if (!residual || !sumsq_out) return QLIN_EINVAL;
-  return qlin::gemv_ep(qweight, qsz, flags, x, bias, residual, y, 1, N, K, bits, group,
-                       kEpResidual, 0, 0, stream, sumsq_out);
-}
-
 extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                              const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,
                              int64_t N, int64_t K, int bits, int group, void* stream) {
   return qlin::gemv_ep(qweight, qsz, flags, x, bias, nullptr, y, M, N, K, bits, group,
                                kEpNone, 0, 0, stream);
 }
+#endif  // QLIN_GEMV_BITS

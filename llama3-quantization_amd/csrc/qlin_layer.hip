@@ -24,7 +24,6 @@
 // + attention_mask, torch.max(w, finfo.min)) with one in-place pass, bit-exact.
 #include "qlin_common.h"
 #include "../../include/qlin_gfx950.h"
-#include "../../include/qlin_gfx950_prefetch.h"
 
 namespace {
 
@@ -375,39 +374,5 @@ extern "C" int qlin_rope_kv_f16(const uint16_t* q, int64_t q_row_stride, const u
   if (B * S == 0) return QLIN_OK;
   hipLaunchKernelGGL(rope_rows_kernel, dim3((unsigned)(B * S)), dim3(256), 0, (hipStream_t)stream,
                      ra);
-  return (int)hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// qlin_prefetch (include/qlin_gfx950_prefetch.h): stream a buffer through plain 16-B loads so it
-// is cache-resident for a following launch; 8 loads in flight per thread.  The XOR of the data
-// feeds a store that never happens for real data (acc == an improbable word AND a zero flag
-// argument), which keeps the loads; the store is a per-lane vector store.
-namespace {
-__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* __restrict__ p, int64_t n16,
-                                                       uint32_t* __restrict__ sink, int never) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  uint32_t acc = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += 8 * stride) {
-    uint4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t j = i + u * stride;
-      v[u] = j < n16 ? p[j] : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-  }
-  if (never && acc == 0x9E3779B9u) sink[threadIdx.x] = acc;
-}
-}  // namespace
-
-extern "C" int qlin_prefetch(const void* p, int64_t bytes, int blocks, void* stream) {
-  if (!p || bytes < 0 || blocks < 0 || (reinterpret_cast<uintptr_t>(p) & 15)) return QLIN_EINVAL;
-  const int64_t n16 = bytes / 16;
-  if (n16 == 0) return QLIN_OK;
-  if (blocks == 0) blocks = qlin::device_cu_count();
-  hipLaunchKernelGGL(prefetch_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                     reinterpret_cast<const uint4*>(p), n16, nullptr, 0);
   return (int)hipGetLastError();
 }

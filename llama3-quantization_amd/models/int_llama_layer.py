@@ -13,7 +13,6 @@ attention matmuls (fp32 attention core, as the reference intends), and the atten
 cast back to the layer's activation dtype before o_proj.  In fp32 this is exactly the reference.
 """
 import math
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -21,32 +20,9 @@ from torch import nn
 
 from quant import qlin
 from quant.int_linear import (FusedPackedLinear, QuantLinear, SiluMulPackedLinear, _same_act,
-                              act_spec, attn_merge_ok, packed_attn_merge_linear,
-                              packed_residual_linear)
+                              act_spec, packed_residual_linear)
 from quant.int_matmul import QuantMatMul
 from quant.omni_norm import KERNEL_MAX_ROWS, OmniLlamaRMSNorm
-
-
-_SIDE_STREAMS = {}
-
-
-def _side_stream(device):
-    """One side stream per device for the decode weight prefetch (forked from and joined back
-    into the caller's stream within one layer step)."""
-    key = device.index
-    s = _SIDE_STREAMS.get(key)
-    if s is None:
-        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device)
-    return s
-
-
-# opt-in decode weight prefetch (QuantLlamaDecoderLayer.fuse_packed_projections): o_proj's and
-# down_proj's packed weights read beside the attention launch
-PREFETCH_DECODE_WEIGHTS = os.environ.get("QLIN_DECODE_PREFETCH", "0") != "0"
-PREFETCH_BLOCKS = int(os.environ.get("QLIN_DECODE_PREFETCH_BLOCKS", "0"))
-# opt-in: o_proj's packed weights read by extra blocks of the decode attention launch itself
-PREFETCH_O_IN_ATTN = os.environ.get("QLIN_ATTN_PREFETCH_O", "0") == "1"
-PREFETCH_O_BLOCKS = int(os.environ.get("QLIN_ATTN_PREFETCH_O_BLOCKS", "128"))
 
 
 def _rope_theta(config):
@@ -321,19 +297,6 @@ class QuantLlamaAttention(nn.Module):
             self._rope32_key = key
         return self._rope32
 
-    def _start_prefetch(self, device):
-        """Opt-in (``prefetch_weights``, set by the decoder layer): the packed weights of the
-        step's next linears read on a side stream beside the latency-bound attention launch, so
-        those launches find them in the memory-side cache; the decoder layer joins the stream."""
-        if not getattr(self, "prefetch_weights", None):
-            return
-        cur = torch.cuda.current_stream(device)
-        side = _side_stream(device)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            qlin.prefetch(*self.prefetch_weights, blocks=PREFETCH_BLOCKS)
-        self._prefetch_stream = side
-
     def _out(self, attn_output, residual):
         if residual is None:
             return self.o_proj(attn_output)
@@ -379,24 +342,11 @@ class QuantLlamaAttention(nn.Module):
             if decode:
                 # one launch: RoPE, the cache append and the decode attention
                 buf, L0 = self._cache_for(past_key_value, bsz, 1, q.device)
-                self._start_prefetch(q.device)
-                merge = bsz == 1 and attn_merge_ok(self.o_proj, L0 + 1, self.num_heads,
-                                                   self.num_key_value_heads, residual, act_dtype)
                 attn_output = qlin.attn_decode_rope(
                     q, k, v, cos_c, sin_c, position_ids, self.num_heads, self.num_key_value_heads,
                     self.head_dim, buf[0], buf[1], L0, attention_mask, math.sqrt(self.head_dim),
-                    out_dtype=act_dtype if act_dtype == torch.float16 else torch.float32,
-                    partials_only=merge,
-                    prefetch=self.o_proj.qweight if PREFETCH_O_IN_ATTN and residual is not None
-                    and getattr(self.o_proj, "packed", False) else None,
-                    prefetch_blocks=PREFETCH_O_BLOCKS)
+                    out_dtype=act_dtype if act_dtype == torch.float16 else torch.float32)
                 past_key_value = (buf[0][:, :, :L0 + 1], buf[1][:, :, :L0 + 1]) if use_cache else None
-                if merge:
-                    # the split-L merge runs inside o_proj (+ residual): one launch fewer round
-                    # trips than attention-merge-then-o_proj, same arithmetic up to fp32 order
-                    return packed_attn_merge_linear(self.o_proj, attn_output, L0 + 1, self.num_heads,
-                                                    self.num_key_value_heads, residual), \
-                        None, past_key_value
                 attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
                 return self._out(attn_output, residual), None, past_key_value
             if kv_mode:
@@ -423,17 +373,10 @@ class QuantLlamaAttention(nn.Module):
                 and qlin.attn_decode_supported(query_states, key_states, attention_mask)):
             # fused decode attention: same fp32 arithmetic as the path below (repeat_kv, QK^T,
             # / sqrt(d), + mask, clamp, softmax, PV) up to summation order
-            L = key_states.shape[2]
-            merge = bsz == 1 and attn_merge_ok(self.o_proj, L, self.num_heads,
-                                               self.num_key_value_heads, residual, act_dtype)
             attn_output = qlin.attn_decode(query_states, key_states, value_states, attention_mask,
                                            math.sqrt(self.head_dim),
                                            out_dtype=act_dtype if act_dtype == torch.float16
-                                           else torch.float32, partials_only=merge)
-            if merge:  # as in the decode branch above
-                return packed_attn_merge_linear(self.o_proj, attn_output, L, self.num_heads,
-                                                self.num_key_value_heads, residual), \
-                    None, past_key_value
+                                           else torch.float32)
             attn_output = attn_output.transpose(1, 2).reshape(bsz, q_len, self.hidden_size).to(act_dtype)
             return self._out(attn_output, residual), None, past_key_value
 
@@ -535,10 +478,6 @@ class QuantLlamaDecoderLayer(nn.Module):
             residual = hidden_states
             hidden_states = self.mlp(hidden_states, residual=residual,
                                      prenorm=self.post_attention_layernorm)
-            side = getattr(self.self_attn, "_prefetch_stream", None)
-            if side is not None:  # join the prefetch stream (graph capture needs it joined)
-                torch.cuda.current_stream(hidden_states.device).wait_stream(side)
-                self.self_attn._prefetch_stream = None
         else:
             hidden_states = self.input_layernorm(hidden_states)
             hidden_states, self_attn_weights, present_key_value = self.self_attn(
@@ -572,11 +511,6 @@ class QuantLlamaDecoderLayer(nn.Module):
         self.self_attn.fuse_packed(prefill_attention, kv_cache)
         self.mlp.fuse_packed()
         self.fused_epilogues = self.self_attn.o_proj.packed and self.mlp.down_proj.packed
-        if self.fused_epilogues and kv_cache and PREFETCH_DECODE_WEIGHTS:
-            o, d = self.self_attn.o_proj, self.mlp.down_proj
-            what = os.environ.get("QLIN_DECODE_PREFETCH", "od")
-            self.self_attn.prefetch_weights = ((o.qweight, o.qsz) if "o" in what else ()) + \
-                ((d.qweight, d.qsz) if "d" in what else ())
         self.input_layernorm.use_kernel = True
         self.post_attention_layernorm.use_kernel = True
         # windows too take the RMSNorm kernel once the attention is no longer bit-exact anyway

@@ -14,8 +14,6 @@ Added (the real-quant path of quant/omniquant.py:315-335, re-done for MI355X):
     RTN quantize + pack of a float weight in one kernel.
   * ``packed`` / ``qweight`` / ``qsz`` / ``qflags`` / ``wbits`` / ``group`` state.
 """
-import os
-
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -314,34 +312,6 @@ class SiluMulPackedLinear(nn.Module):
                            self.qflags, epilogue=qlin.EP_SILU_MUL, act_bits=act[0],
                            act_flags=act[1])
         return y if x.dtype == torch.float16 else y.to(x.dtype)
-
-
-# the decode attention's split-L merge inside o_proj (qlin_attn_merge_linear_f16), opt-in: every
-# o_proj block re-reads all S partials (S x 2 the bytes of x: 147 KB per block, 38 MB of L2 reads
-# per launch at L = 513), which costs more than the attention launch's merge round trips it
-# removes — decode layer 43.1 vs 42.0 us at L = 513 (profiles/r3_attn_merge_o_proj_ab.txt)
-MERGE_INTO_O_PROJ = os.environ.get("QLIN_ATTN_MERGE_O_PROJ", "0") == "1"
-
-
-def attn_merge_ok(lin, L, n_heads, n_kv_heads, residual, act_dtype):
-    """Whether ``residual + lin(attn)`` of a one-token decode step over L cache rows can take the
-    attention's split partials straight into ``lin`` (``packed_attn_merge_linear``)."""
-    return (MERGE_INTO_O_PROJ and residual is not None and act_dtype == torch.float16
-            and residual.dtype == torch.float16 and residual.numel() == lin.out_features
-            and getattr(lin, "packed", False) and act_spec(lin) == (0, 0)
-            and lin.in_features == n_heads * qlin.ATTN_D
-            and qlin.attn_merge_linear_supported(L, n_heads, n_kv_heads, lin.out_features,
-                                                 lin.wbits, lin.group, lin.qflags))
-
-
-def packed_attn_merge_linear(lin, partials, L, n_heads, n_kv_heads, residual):
-    """``residual + lin(attn)`` with attn the merged split-L partials of the decode attention
-    launch (``attn_merge_ok``): the merge, the fp16 rounding of attn, o_proj and the residual
-    add in one launch."""
-    bias = None if lin.bias is None else lin.bias.to(torch.float16).contiguous()
-    return qlin.attn_merge_linear(partials, L, n_heads, n_kv_heads, lin.qweight, lin.qsz, bias,
-                                  residual.contiguous(), lin.out_features, lin.wbits, lin.group,
-                                  lin.qflags)
 
 
 def packed_residual_linear(lin, x, residual):

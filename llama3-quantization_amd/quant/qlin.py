@@ -10,13 +10,14 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 
 import torch
 
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -58,8 +59,7 @@ SIGNATURES = {
                                _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p], _i),
     "qlin_rmsnorm_linear_supported": ([_l, _l, _l, _i, _i], _i),
     "qlin_rmsnorm_linear_ep_f16": ([_p, _p, _i, _p, _p, ctypes.c_float, _p, _p, _p, _l, _l, _l,
-                                    _i, _i, _i, _p, _l, _p, _p, _p, _l, _p, _p], _i),
-    "qlin_linear_res_sumsq_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _i, _i, _p, _p], _i),
+                                    _i, _i, _i, _p], _i),
     "qlin_rope_kv_f16": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _p, _l, _l, _l, _l,
                           _i, _i, _i, _p], _i),
     "qlin_attn_scores_f32": ([_p, _p, _i, _l, _l, _l, _l, _l, ctypes.c_float, _p], _i),
@@ -70,16 +70,6 @@ SIGNATURES = {
                           _p],
                          _i),
     "qlin_attn_decode_splits": ([_l, _i, _l], _i),
-    "qlin_attn_merge_linear_supported": ([_l, _i, _i, _l, _i, _i, _i], _i),
-    "qlin_attn_merge_linear_f16": ([_p, _l, _i, _i, _p, _p, _i, _p, _p, _p, _l, _i, _i, _p], _i),
-    "qlin_prefetch": ([_p, _l, _i, _p], _i),
-    "qlin_attn_decode_rope_pf": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _p, _p,
-                                  _i, _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p, _p, _l, _i],
-                                 _i),
-    "qlin_decode_supported": ([_i, _l, _l, _i, _i, _i, _i, _i, _i], _i),
-    "qlin_decode_workspace_bytes": ([_i, _l, _l, _i, _i, _i, _l], _l),
-    "qlin_decode_llama_f16": ([_p, _i, _l, _l, _i, _i, _i, _i, _i, _i, ctypes.c_float, _p, _p, _p,
-                               _p, _l, _p, _l, _l, _p, ctypes.c_float, _p, _l, _p], _i),
 }
 
 
@@ -425,14 +415,12 @@ def rmsnorm_linear_supported(M, N, K, bits, group):
 
 
 def rmsnorm_linear_ep(x, norm_weight, eps, qweight, qsz, bias, N, K, bits, group, flags=0,
-                      epilogue=EP_NONE, residual=None, sumsq=None, rope=None):
+                      epilogue=EP_NONE, residual=None):
     """``qlin_rmsnorm_linear_ep_f16``: ``linear_ep(rmsnorm(x))`` for one token row in ONE launch —
     x fp16 [.., K] is the hidden state BEFORE the RMSNorm (norm_weight fp32 [K], eps), which the
-    GEMV applies to its x words itself (the sum of squares in another order than ``rmsnorm``:
-    the normed x can differ from it by an fp16 ulp).  ``sumsq``: fp32 [ceil(K/16)] partial sums of
-    squares of x written by ``linear_res_sumsq`` (precomputed statistics); ``rope``: (position_ids,
-    cos fp32 [rows, 128], sin, out fp32 [256]) — the launch also copies that position's cos / sin
-    rows into ``out`` for ``attn_decode_rope(..., position_ids=None)``."""
+    kernel applies at the reference's rounding point, RN16(w * (x * rsqrt(mean(x^2) + eps)))
+    (the sum of squares in another order than ``rmsnorm``: an fp16 ulp of the normed x can
+    differ from it)."""
     _dev(x, qweight, qsz, bias, residual, norm_weight)
     if x.dtype != torch.float16 or norm_weight.dtype != torch.float32:
         raise ValueError("rmsnorm_linear_ep takes fp16 x and an fp32 norm weight")
@@ -449,49 +437,10 @@ def rmsnorm_linear_ep(x, norm_weight, eps, qweight, qsz, bias, N, K, bits, group
     if epilogue == EP_RESIDUAL:
         if residual is None or residual.dtype != torch.float16 or residual.shape != y.shape:
             raise ValueError(f"residual must be fp16 {tuple(y.shape)}")
-    sq_n = 0
-    if sumsq is not None:
-        _on_gpu(sumsq)
-        if sumsq.dtype != torch.float32 or sumsq.numel() != (K + 15) // 16 or \
-                not sumsq.is_contiguous():
-            raise ValueError(f"sumsq must be fp32 [{(K + 15) // 16}]")
-        sq_n = sumsq.numel()
-    rp = rc_ = rs_ = ro = None
-    rows = 0
-    if rope is not None:
-        rp, rc_, rs_, ro = rope
-        _on_gpu(rp, rc_, rs_, ro)
-        if ro.dtype != torch.float32 or ro.numel() < 256 or rc_.dtype != torch.float32 or \
-                rs_.dtype != torch.float32 or not (rc_.is_contiguous() and rs_.is_contiguous()):
-            raise ValueError("rope: fp32 cos / sin caches and an fp32 [256] output")
-        rp = rp.reshape(-1)[:1].to(torch.int64).contiguous()
-        rows = rc_.shape[0]
     rc = load_library().qlin_rmsnorm_linear_ep_f16(
         _ptr(qweight), _ptr(qsz), flags, _ptr(x), _ptr(norm_weight), float(eps), _ptr(bias),
-        _ptr(residual), _ptr(y), M, N, K, bits, group, epilogue, _ptr(sumsq), sq_n, _ptr(rp),
-        _ptr(rc_), _ptr(rs_), rows, _ptr(ro), _stream(x))
+        _ptr(residual), _ptr(y), M, N, K, bits, group, epilogue, _stream(x))
     _check(rc, "qlin_rmsnorm_linear_ep_f16")
-    return y
-
-
-def linear_res_sumsq(x, qweight, qsz, bias, N, K, bits, group, flags, residual, sumsq_out):
-    """``qlin_linear_res_sumsq_f16``: one token row ``residual + F.linear(x)`` that also writes
-    ``sumsq_out`` (fp32 [ceil(N/16)]: per 16 outputs, the sum of their squares) — the statistics
-    of the RMSNorm that reads the output next (``rmsnorm_linear_ep(..., sumsq=...)``)."""
-    _dev(x, qweight, qsz, bias, residual, sumsq_out)
-    if x.dtype != torch.float16 or x.shape[-1] != K or x.numel() != K:
-        raise ValueError(f"linear_res_sumsq takes one fp16 row of {K} features")
-    _check_packed(qweight, qsz, N, K, bits, group)
-    y = torch.empty(*x.shape[:-1], N, dtype=torch.float16, device=x.device)
-    if residual is None or residual.dtype != torch.float16 or residual.shape != y.shape:
-        raise ValueError(f"residual must be fp16 {tuple(y.shape)}")
-    if sumsq_out.dtype != torch.float32 or sumsq_out.numel() != (N + 15) // 16:
-        raise ValueError(f"sumsq_out must be fp32 [{(N + 15) // 16}]")
-    b = None if bias is None else bias.to(torch.float16).contiguous()
-    rc = load_library().qlin_linear_res_sumsq_f16(
-        _ptr(qweight), _ptr(qsz), flags, _ptr(x.contiguous()), _ptr(b), _ptr(residual.contiguous()),
-        _ptr(y), N, K, bits, group, _ptr(sumsq_out), _stream(x))
-    _check(rc, "qlin_linear_res_sumsq_f16")
     return y
 
 
@@ -680,12 +629,11 @@ def _cache_head_stride(k, v):
     return hs
 
 
-def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32, partials_only=False):
+def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32):
     """softmax(q k^T / scale_div + mask) v for one query token: q fp32 [B, Hq, 1, D], k/v fp16
     [B, Hkv, L, D], mask fp16 [B, 1, 1, L] or None -> [B, Hq, 1, D] in out_dtype (fp32, or the
     fp32 result rounded to fp16 in the kernel); k / v may be row-prefix views of KV cache
-    buffers (rope_kv), read in place.  partials_only (``attn_merge_linear_supported``): returns
-    the split-L partials for ``attn_merge_linear`` instead (no merge in this launch)."""
+    buffers (rope_kv), read in place."""
     _on_gpu(q, k, v)
     if not attn_decode_supported(q, k, mask):
         raise ValueError("attn_decode: unsupported shapes / dtypes")
@@ -702,80 +650,33 @@ def attn_decode(q, k, v, mask, scale_div, out_dtype=torch.float32, partials_only
             mask.expand(B, 1, 1, L).reshape(B, L).contiguous()
     out = torch.empty(B, Hq, 1, D, dtype=out_dtype, device=q.device)
     lib = load_library()
-    part, cnt = _attn_partials(lib, q.device, B, Hq, Hkv, L, partials_only)
+    part, cnt = _attn_partials(lib, q.device, B, Hq, Hkv, L)
     rc = lib.qlin_attn_decode(_ptr(q.contiguous()), _ptr(k), _ptr(v), _ptr(m), _ptr(out),
                               _dtcode(out),
                               B, Hq, Hkv, L, D, hs, float(scale_div), _ptr(part), _ptr(cnt),
                               _stream(q))
     _check(rc, "qlin_attn_decode")
-    return part if partials_only else out
+    return out
 
 
-def _attn_partials(lib, device, B, Hq, Hkv, L, partials_only):
-    """(partials scratch, merge counters) of a decode attention launch; partials_only: counters
-    None (the launch stops after writing the partials)."""
+def _attn_partials(lib, device, B, Hq, Hkv, L):
+    """(partials scratch, merge counters) of a decode attention launch."""
     nbytes = lib.qlin_attn_decode_partials_bytes(B, Hq, Hkv, L)
     if nbytes < 0:
         raise ValueError("attn_decode: unsupported shapes")
-    if partials_only and (B != 1 or nbytes == 0):
-        raise ValueError("attn_decode partials_only: batch 1 with a split cache (see "
-                         "attn_merge_linear_supported)")
     if not nbytes:
         return None, None
     part = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
-    return part, (None if partials_only else _attn_counters(device, B * Hkv))
-
-
-def prefetch(*tensors, blocks=0):
-    """``qlin_prefetch`` (include/qlin_gfx950_prefetch.h): read each tensor once on the current
-    stream so it is cache-resident for a later launch (weights of the next linears, issued on a
-    side stream beside a latency-bound launch).  Changes no data."""
-    lib = load_library()
-    for t_ in tensors:
-        _dev(t_)
-        _check(lib.qlin_prefetch(_ptr(t_), t_.numel() * t_.element_size(), blocks, _stream(t_)),
-               "qlin_prefetch")
-
-
-def attn_merge_linear_supported(L, Hq, Hkv, N, bits, group, flags=0):
-    """Whether ``attn_merge_linear`` takes a decode step over L cache rows (batch 1)."""
-    return bool(load_library().qlin_attn_merge_linear_supported(L, Hq, Hkv, N, bits, group, flags))
-
-
-def attn_merge_linear(partials, L, Hq, Hkv, qweight, qsz, bias, residual, N, bits, group,
-                      flags=0):
-    """``qlin_attn_merge_linear_f16``: ``residual + o_proj(attn)`` for one decode token, attn the
-    split-L partials of ``attn_decode(..., partials_only=True)`` (or ``attn_decode_rope``) merged
-    and rounded to fp16 inside the o_proj launch.  residual fp16 [.., N] (one row) -> y like it."""
-    _dev(partials, qweight, qsz, bias, residual)
-    K = Hq * ATTN_D
-    _check_packed(qweight, qsz, N, K, bits, group)
-    if residual.dtype != torch.float16 or residual.numel() != N:
-        raise ValueError(f"residual must be one fp16 row of {N}")
-    if bias is not None and (bias.dtype != torch.float16 or bias.numel() != N):
-        raise ValueError("bias must be fp16 [N]")
-    lib = load_library()
-    need = lib.qlin_attn_decode_partials_bytes(1, Hq, Hkv, L)
-    if partials.dtype != torch.float32 or partials.numel() * 4 < need or need <= 0:
-        raise ValueError("partials: the fp32 scratch of attn_decode(partials_only=True)")
-    y = torch.empty_like(residual)
-    rc = lib.qlin_attn_merge_linear_f16(_ptr(partials), L, Hq, Hkv, _ptr(qweight), _ptr(qsz),
-                                        flags, _ptr(bias), _ptr(residual), _ptr(y), N, bits,
-                                        group, _stream(residual))
-    _check(rc, "qlin_attn_merge_linear_f16")
-    return y
+    return part, _attn_counters(device, B * Hkv)
 
 
 def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim,
-                     k_cache, v_cache, kv0, mask, scale_div, out_dtype=torch.float32,
-                     partials_only=False, prefetch=None, prefetch_blocks=128):
+                     k_cache, v_cache, kv0, mask, scale_div, out_dtype=torch.float32):
     """``qlin_attn_decode_rope``: ``rope_kv`` + ``attn_decode`` in one launch for one new token:
     q [B, 1, Hq*D], k / v [B, 1, Hkv*D] fp16 row-strided views (before RoPE); k_cache / v_cache
     fp16 [B, Hkv, rows, D] contiguous buffers holding rows 0 .. kv0 - 1, row kv0 written here;
     mask fp16 [B, 1, 1, kv0 + 1] or None -> [B, Hq, 1, D] (out_dtype), bit-identical to the two
-    launches.  partials_only: the split-L partials for ``attn_merge_linear`` instead.
-    prefetch: a contiguous device tensor (the next launch's packed weights) read by
-    ``prefetch_blocks`` extra blocks of the same launch (``qlin_attn_decode_rope_pf``)."""
+    launches."""
     for t_ in (q, k, v):
         if _rows(t_) is None:
             raise ValueError("attn_decode_rope takes row-strided [B, 1, H*D] q / k / v")
@@ -811,21 +712,15 @@ def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_
             mask.expand(B, 1, 1, L).reshape(B, L).contiguous()
     out = torch.empty(B, n_heads, 1, head_dim, dtype=out_dtype, device=q.device)
     lib = load_library()
-    part, cnt = _attn_partials(lib, q.device, B, n_heads, n_kv_heads, L, partials_only)
+    part, cnt = _attn_partials(lib, q.device, B, n_heads, n_kv_heads, L)
     rows = k_cache.shape[2]
     args = (_ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(v), _rows(v), _ptr(cos_cache),
             _ptr(sin_cache), cos_cache.shape[0], _ptr(pos), pbs, _ptr(k_cache), _ptr(v_cache),
             rows * head_dim, _ptr(m), _ptr(out), _dtcode(out), B, n_heads, n_kv_heads, L, head_dim,
             float(scale_div), _ptr(part), _ptr(cnt), _stream(q))
-    if prefetch is not None:
-        _dev(prefetch)
-        rc = lib.qlin_attn_decode_rope_pf(*args, _ptr(prefetch),
-                                          prefetch.numel() * prefetch.element_size(),
-                                          prefetch_blocks)
-    else:
-        rc = lib.qlin_attn_decode_rope(*args)
+    rc = lib.qlin_attn_decode_rope(*args)
     _check(rc, "qlin_attn_decode_rope")
-    return part if partials_only else out
+    return out
 
 
 def attn_prefill_supported(q, k, mask=None):
@@ -840,7 +735,7 @@ def attn_prefill_supported(q, k, mask=None):
                                   and mask.dtype in (torch.float16, torch.float32))))
 
 
-_CAUSAL = []  # [(mask tensor, its _version, S, L, result)], most recent last
+_CAUSAL = []  # [(weakref to the mask tensor, its _version, S, L, result)], most recent last
 _CAUSAL_KEEP = 4
 
 
@@ -849,10 +744,11 @@ def mask_is_causal(mask, S, L) -> int:
     (key > L - S + i) at <= -1e4 (so its exp() underflows to 0) and keeps some key of every row
     open, 2 if moreover every key on and below the diagonal is exactly 0 (the pure causal
     pattern), else 0.  Cached per tensor OBJECT and version (one check per forward: the decoder
-    layers share the mask): the cache holds the mask itself and matches it with ``is``, so a new
-    mask that the allocator places at a freed mask's address is never taken for it."""
+    layers share the mask): the cache holds a weak reference to the mask and matches it with
+    ``is``, so a new mask that the allocator places at a freed mask's address is never taken for
+    it, and a cached mask's memory is freed with its last user."""
     for ent in _CAUSAL:
-        if ent[0] is mask and ent[1] == mask._version and ent[2] == S and ent[3] == L:
+        if ent[0]() is mask and ent[1] == mask._version and ent[2] == S and ent[3] == L:
             return ent[4]
     i = torch.arange(S, device=mask.device)[:, None]
     j = torch.arange(L, device=mask.device)[None, :]
@@ -862,7 +758,7 @@ def mask_is_causal(mask, S, L) -> int:
     ok = int(bool((m[:, above] <= -1e4).all()) and bool((open_max > -1e4).all()))
     if ok and bool((m[:, ~above] == 0).all()):
         ok = 2
-    _CAUSAL.append((mask, mask._version, S, L, ok))
+    _CAUSAL.append((weakref.ref(mask), mask._version, S, L, ok))
     del _CAUSAL[:-_CAUSAL_KEEP]
     return ok
 
@@ -896,32 +792,3 @@ def attn_prefill(q, k, v, mask, scale_div, out_dtype=torch.float32):
                                           float(scale_div), _stream(q))
     _check(rc, "qlin_attn_prefill")
     return out
-
-
-# ---------------------------------------------------------------------------------------------
-# persistent decode engine (qlin_decode_llama_f16)
-# ---------------------------------------------------------------------------------------------
-DECODE_LAYER_PTRS = 12  # qlin_decode_layer: 4 qweight, 4 qsz, 2 norm weights, 2 caches
-
-
-def decode_supported(n_layers, H, I, Hq, Hkv, D, bits, group, flags) -> bool:
-    return bool(load_library().qlin_decode_supported(n_layers, H, I, Hq, Hkv, D, bits, group,
-                                                     flags))
-
-
-def decode_workspace_bytes(n_layers, H, I, Hq, Hkv, D, max_L) -> int:
-    return int(load_library().qlin_decode_workspace_bytes(n_layers, H, I, Hq, Hkv, D, max_L))
-
-
-def decode_llama(table, n_layers, H, I, Hq, Hkv, D, bits, group, flags, eps, x, y, cos_cache,
-                 sin_cache, position, L0, kv_rows, mask, scale_div, workspace):
-    """``qlin_decode_llama_f16``: one decode step through ``n_layers`` layers in one launch.
-    ``table`` int64 [n_layers, 12] device tensor of qlin_decode_layer pointers; x / y fp16 [H];
-    position int64 device scalar; mask fp16 [L0 + 1] or None; workspace uint8 device buffer."""
-    _on_gpu(table, x, y, cos_cache, sin_cache, position, mask, workspace)
-    rc = load_library().qlin_decode_llama_f16(
-        _ptr(table), n_layers, H, I, Hq, Hkv, D, bits, group, flags, float(eps), _ptr(x), _ptr(y),
-        _ptr(cos_cache), _ptr(sin_cache), cos_cache.shape[0], _ptr(position), L0, kv_rows,
-        _ptr(mask), float(scale_div), _ptr(workspace), workspace.numel(), _stream(x))
-    _check(rc, "qlin_decode_llama_f16")
-    return y

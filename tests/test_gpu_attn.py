@@ -118,143 +118,6 @@ def test_attn_decode_rope_equals_two_launches(B, Hq, Hkv, kv0, rows, masked):
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("Hq,Hkv,L,N,bits,group,biased",
-                         [(32, 8, 513, 4096, 4, 128, False), (32, 8, 200, 1024, 2, 64, True),
-                          (16, 2, 640, 2048, 3, 128, False), (64, 8, 300, 1024, 8, 256, True),
-                          (8, 8, 129, 520, 4, 64, False), (32, 8, 97, 4096, 4, 128, False)])
-def test_attn_merge_linear_matches_two_launches(Hq, Hkv, L, N, bits, group, biased):
-    """qlin_attn_merge_linear_f16 (the split-L merge inside o_proj + residual) vs the attention
-    launch's own merge (out fp16) then qlin_linear_ep_f16(EP_RESIDUAL): both anchored on fp64 —
-    attention in fp64, rounded to fp16 (the layer's .to(fp16)), x the dequantized weight in fp64,
-    rounded to fp16, + residual.  The merged path reorders the fp32 merge only: its error must
-    stay within the two-launch path's plus one fp16 ulp of the output."""
-    from helpers import rand_weight
-    D = 128
-    K = Hq * D
-    S = qlin.load_library().qlin_attn_decode_splits(1, Hkv, L)
-    assert 2 <= S <= 10 and qlin.attn_merge_linear_supported(L, Hq, Hkv, N, bits, group)
-    g = torch.Generator(device="cuda").manual_seed(L + N)
-    q = torch.randn(1, Hq, 1, D, device="cuda", generator=g) * 0.5
-    k = torch.randn(1, Hkv, L, D, device="cuda", generator=g).half()
-    v = torch.randn(1, Hkv, L, D, device="cuda", generator=g).half()
-    mask = torch.zeros(1, 1, 1, L, device="cuda", dtype=torch.float16)
-    mask[..., : L // 5] = torch.finfo(torch.float16).min
-    o = qlin.quantize(torch.from_numpy(rand_weight(N, K, 3)).cuda(), bits, group, 0,
-                      want_xdq=False, want_params=False, pack=True)
-    qw, qsz, fl = o["qweight"], o["qsz"], o["flags"]
-    bias = (torch.randn(N, device="cuda", generator=g) * 0.1).half() if biased else None
-    res = torch.randn(1, 1, N, device="cuda", generator=g).half()
-    part = qlin.attn_decode(q, k, v, mask, math.sqrt(D), out_dtype=torch.float16,
-                            partials_only=True)
-    got = qlin.attn_merge_linear(part, L, Hq, Hkv, qw, qsz, bias, res, N, bits, group, fl)
-    a16 = qlin.attn_decode(q, k, v, mask, math.sqrt(D), out_dtype=torch.float16)
-    two = qlin.linear_ep(a16.reshape(1, 1, K), qw, qsz, bias, N, K, bits, group, fl,
-                         epilogue=qlin.EP_RESIDUAL, residual=res)
-    w64 = qlin.dequant(qw, qsz, N, K, bits, group, fl).double()
-    x64 = _ref(q, k, v, mask).reshape(1, K).half().double()
-    lin = x64 @ w64.T + (bias.double() if biased else 0)
-    y64 = res.reshape(1, N).double() + lin.half().double()
-    e_got = (got.reshape(1, N).double() - y64).abs().max().item()
-    e_two = (two.reshape(1, N).double() - y64).abs().max().item()
-    ulp = 2.0 ** (math.floor(math.log2(y64.abs().max().item())) - 10)
-    assert e_got <= e_two + ulp, (e_got, e_two, ulp)
-    # and most outputs agree with the two-launch path bit for bit
-    assert (got == two).float().mean().item() > 0.9
-    # graph replay: the partials-only launch keeps no counters, replays repeat
-    s_ = torch.cuda.Stream()
-    s_.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s_):
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr, stream=s_):
-            p2 = qlin.attn_decode(q, k, v, mask, math.sqrt(D), partials_only=True)
-            y2 = qlin.attn_merge_linear(p2, L, Hq, Hkv, qw, qsz, bias, res, N, bits, group, fl)
-        for _ in range(2):
-            gr.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(y2, got)
-
-
-def test_layer_decode_with_merge_into_o_proj(monkeypatch):
-    """The opt-in decode path (QLIN_ATTN_MERGE_O_PROJ=1: attention partials only, merged inside
-    the o_proj + residual launch) vs the default path on the same fused kv_cache layer: the same
-    hidden state up to the merge's fp32 order (an fp16 ulp of the attention output here and there),
-    and the same cache rows."""
-    from transformers import LlamaConfig
-    from models.int_llama_layer import QuantLlamaDecoderLayer
-    from models.quant_llama import quant_args, random_llama_layer
-    from quant import int_linear
-    from quant.utils import pack_quant_linears
-    cfg = LlamaConfig(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
-                      num_key_value_heads=2, num_hidden_layers=1, vocab_size=100,
-                      max_position_embeddings=2048, rms_norm_eps=1e-5, rope_theta=500000.0)
-    layer = QuantLlamaDecoderLayer(cfg, random_llama_layer(cfg, 9, "cuda", torch.float16),
-                                   quant_args(4, 128))
-    layer.half()
-    layer.smooth_and_quant_inplace()
-    layer.register_scales_and_zeros()
-    pack_quant_linears(layer)
-    layer.fuse_packed_projections(kv_cache=True)
-    gen = torch.Generator(device="cuda").manual_seed(4)
-    L0 = 400
-    assert qlin.attn_merge_linear_supported(L0 + 1, 8, 2, 1024, 4, 128, layer.self_attn.o_proj.qflags)
-    past = (torch.randn(1, 2, L0, 128, device="cuda", generator=gen).half(),
-            torch.randn(1, 2, L0, 128, device="cuda", generator=gen).half())
-    x = torch.randn(1, 1, 1024, device="cuda", generator=gen).half()
-    pos = torch.tensor([[L0]], device="cuda")
-    import models.int_llama_layer as ill
-    calls = []
-    real = ill.packed_attn_merge_linear
-    monkeypatch.setattr(ill, "packed_attn_merge_linear",
-                        lambda *a: calls.append(1) or real(*a))
-    outs = []
-    for on in (False, True):
-        monkeypatch.setattr(int_linear, "MERGE_INTO_O_PROJ", on)
-        with torch.no_grad():  # past is adopted into fresh cache buffers by each call
-            o = layer(x, position_ids=pos, past_key_value=past, use_cache=True)
-        outs.append((o[0].clone(), o[-1][0].clone(), o[-1][1].clone()))
-    assert len(calls) == 1  # the merged path ran for the second step only
-    (y0, k0, v0), (y1, k1, v1) = outs
-    assert torch.equal(k0, k1) and torch.equal(v0, v1)
-    rel = ((y1.float() - y0.float()).abs().max() / y0.float().abs().max()).item()
-    assert rel < 2e-3, rel
-    assert (y1 == y0).float().mean().item() > 0.9
-
-
-def test_attn_merge_linear_rejects_unsupported():
-    # one split (short cache) or too many (long cache): the attention launch merges itself
-    assert not qlin.attn_merge_linear_supported(40, 32, 8, 4096, 4, 128)
-    assert not qlin.attn_merge_linear_supported(4096, 32, 8, 4096, 4, 128)
-    q = torch.randn(1, 32, 1, 128, device="cuda")
-    k = torch.randn(1, 8, 40, 128, device="cuda").half()
-    with pytest.raises(ValueError):
-        qlin.attn_decode(q, k, k, None, 8.0, partials_only=True)
-
-
-@pytest.mark.parametrize("kv0,blocks", [(512, 128), (40, 8), (300, 64)])
-def test_attn_decode_rope_prefetch_blocks_change_nothing(kv0, blocks):
-    """qlin_attn_decode_rope_pf: the extra prefetch blocks of the launch leave the attention output
-    and the written cache rows bit-identical."""
-    from models.int_llama_layer import LlamaRotaryEmbedding437
-    B, Hq, Hkv, D, rows = 1, 32, 8, 128, 1024
-    g = torch.Generator(device="cuda").manual_seed(kv0)
-    qkv = (torch.randn(B, 1, (Hq + 2 * Hkv) * D, device="cuda", generator=g) * 2).half()
-    q, k, v = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
-    rot = LlamaRotaryEmbedding437(D, 8192, 500000.0, device="cuda").half()
-    cos, sin = rot.cos_cached.float().contiguous(), rot.sin_cached.float().contiguous()
-    pos = torch.full((B, 1), kv0, device="cuda", dtype=torch.int64)
-    kc = torch.randn(B, Hkv, rows, D, device="cuda", generator=g).half()
-    vc = torch.randn(B, Hkv, rows, D, device="cuda", generator=g).half()
-    kc2, vc2 = kc.clone(), vc.clone()
-    w = torch.randint(-2**31, 2**31 - 1, (4096, 512), dtype=torch.int32, device="cuda")
-    a = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, kv0, None, math.sqrt(D),
-                              out_dtype=torch.float16)
-    b = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc2, vc2, kv0, None,
-                              math.sqrt(D), out_dtype=torch.float16, prefetch=w,
-                              prefetch_blocks=blocks)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b) and torch.equal(kc, kc2) and torch.equal(vc, vc2)
-
-
 def test_attn_decode_rejects_unsupported():
     q = torch.randn(1, 32, 1, 64, device="cuda")
     k = torch.randn(1, 8, 10, 64, device="cuda").half()

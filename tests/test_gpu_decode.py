@@ -1,24 +1,30 @@
 """Full-width parity (north_star: logits within 1e-3 relative of the reference fake-quant path) at
-LLaMA3-8B shapes: hidden 4096, intermediate 14336, 32 query / 8 KV heads, vocab 128,256, four
-decoder layers (reference models/int_llama_layer.py:103-179 and :213-267, quant/int_linear.py:62).
+LLaMA3-8B shapes: hidden 4096, intermediate 14336, 32 query / 8 KV heads, vocab 128,256
+(reference models/int_llama_layer.py:103-179 and :213-267, quant/int_linear.py:62,
+quant/omni_norm.py:52-63).
 
-Three-way comparison.  Every fp16 path is measured against a float64 evaluation of the same layer
-mathematics on the same W_dq, KV cache and input (``_ref64_*`` below: no intermediate roundings):
+Every fp16 path runs the same random-init stack on the same W_dq, KV cache and input:
   fake_quant          the reference's path: dense fp16 F.linear on W_dq + the reference's torch glue;
   fake_quant_f32lin   the SAME reference arithmetic with F.linear run on fp32 copies of the fp16
-                      operands (another summation order of the same fp32-accumulated products,
-                      rounded to fp16 the same way): the order-sensitivity floor of the stack;
+                      operands (the same fp32-accumulated products in another summation order,
+                      rounded to fp16 the same way): the reference against itself, the order floor;
   packed              the gfx950 packed linears (QuantLinear packed mode), reference torch glue;
   fused_*             the fused packed layer (fuse_packed_projections) — decode with the KV cache
-                      appended in place; prefill with the fused attention kernel.
-On random-init stacks an fp16 ulp flip anywhere is amplified layer after layer, so two correct
-fp16 paths — the reference against itself with another F.linear order included — differ from each
-other by more than 1e-3 of max |logit|.  The criteria are therefore:
-  * no packed path is measurably less accurate against fp64 than the reference's own fp16
-    arithmetic (err_vs_fp64 <= 1.25 x fake_quant's + 1e-4);
-  * its distance to the fake-quant logits stays within the distance between the reference and
-    its own reordered twin (<= max(1e-3, 1.5 x floor)).
-Numbers are written to $QLIN_PARITY_OUT (profiles/r3_decode_parity.json, r3_prefill_parity.json)."""
+                      appended in place (RMSNorm inside the q/k/v and gate/up launches, attention +
+                      RoPE + append in one launch, residual / SiLU epilogues); prefill with the
+                      fused prefill-attention kernel.
+Logits are formed from each path's final hidden state by a float64 head (the model's RMSNorm and
+lm_head in fp64), so fp16 rounding of the logits themselves does not dominate the comparison, and
+are compared with the fake-quant path's: max |diff| / max |logit| (``max``), the 99th percentile
+of |diff| / max |logit| (``p99``) and top-1 agreement.  A float64 evaluation of the same layer
+mathematics (no intermediate roundings) anchors accuracy.
+
+On random-init stacks an fp16 ulp flip anywhere is amplified layer after layer: the reference
+differs from its own reordered twin by more than 1e-3 of max |logit| (the order floor).  The bar
+ on every seed: each packed / fused path's max and p99 distance to the
+fake-quant logits <= 1.1 x the floor's, and its error against float64 <= 1.1 x the reference's.
+Numbers are written to $QLIN_PARITY_OUT (profiles/r4_decode_parity.json, r4_prefill_parity.json,
+r4_prefill32_parity.json)."""
 import json
 import math
 import os
@@ -37,12 +43,14 @@ from quant.utils import pack_quant_linears  # noqa: E402
 
 LAYERS = 4
 KV = 512
+SEEDS = (21, 31, 41)
+BAR = 1.1
 
 
-def _cfg():
+def _cfg(layers=LAYERS):
     from transformers import LlamaConfig
     return LlamaConfig(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
-                       num_key_value_heads=8, num_hidden_layers=LAYERS, vocab_size=128256,
+                       num_key_value_heads=8, num_hidden_layers=layers, vocab_size=128256,
                        max_position_embeddings=8192, rms_norm_eps=1e-5, rope_theta=500000.0)
 
 
@@ -111,8 +119,21 @@ def _ref64_window(layer, h, cfg):
     return _mlp64(layer, h + a @ W(at.o_proj).T, eps)
 
 
-def _rel(a, b):
-    return ((a.double() - b.double()).abs().max() / b.double().abs().max()).item()
+def _head64(model, h, cfg):
+    """The model's RMSNorm + lm_head in float64 on a final hidden state."""
+    return _rms64(h.double(), model.norm.weight.double(), cfg.rms_norm_eps) @ \
+        model.lm_head.weight.double().T
+
+
+def _stats(lg, ref):
+    """max / p99 of |lg - ref| relative to max |ref|, and top-1 agreement (fraction of rows)."""
+    d = (lg - ref).abs().reshape(-1)
+    scale = ref.abs().max()
+    k = max(1, int(math.ceil(0.99 * d.numel())))
+    p99 = d.float().kthvalue(k).values.double() if d.numel() > 1 else d.max()
+    top1 = (lg.reshape(-1, lg.shape[-1]).argmax(-1) == ref.reshape(-1, ref.shape[-1]).argmax(-1))
+    return {"max": (d.max() / scale).item(), "p99": (p99 / scale).item(),
+            "top1": top1.double().mean().item()}
 
 
 def _f32_linear(x, w, b=None):
@@ -127,34 +148,68 @@ def _reorder_reference(model, on):
             m.fwd_func = _f32_linear if on else F.linear
 
 
-def _judge(rep, paths, ref_name="fake_quant", floor_name="fake_quant_f32lin"):
-    fq = rep[ref_name]["logits_err_vs_fp64"]
-    floor = rep[floor_name]["logits_rel_vs_fake_quant"]
-    rep["criteria"] = {"err_vs_fp64_max": 1.25 * fq + 1e-4,
-                       "rel_vs_fake_quant_max": max(1e-3, 1.5 * floor),
-                       "order_floor": floor}
-    out = os.environ.get("QLIN_PARITY_OUT")
+def _progress(*a):
+    print("[parity]", *a, flush=True)  # a long full-width case shows it is alive
+
+
+def _report(seed, paths, model, cfg, ref64_h):
+    logits64 = _head64(model, ref64_h, cfg)
+    ref = _head64(model, paths["fake_quant"], cfg)
+    rep = {"seed": seed}
+    for name, h in paths.items():
+        lg = _head64(model, h, cfg)
+        r = {"logits_err_vs_fp64": _stats(lg, logits64)["max"],
+             "hidden_err_vs_fp64": ((h.double() - ref64_h).abs().max()
+                                    / ref64_h.abs().max()).item()}
+        r.update({f"logits_{k}_vs_fake_quant": v for k, v in _stats(lg, ref).items()})
+        r["hidden_rel_vs_fake_quant"] = ((h.double() - paths["fake_quant"].double()).abs().max()
+                                         / paths["fake_quant"].double().abs().max()).item()
+        rep[name] = r
+    return rep
+
+
+def _judge(reps, ref_name="fake_quant", floor_name="fake_quant_f32lin", out_env=None):
+    """Per seed: every other path within BAR x the order floor (max and p99) and BAR x the
+    reference's own float64 error."""
+    failures = []
+    for rep in reps:
+        fl = rep[floor_name]
+        fq = rep[ref_name]
+        crit = {"max_vs_fake_quant": BAR * fl["logits_max_vs_fake_quant"],
+                "p99_vs_fake_quant": BAR * fl["logits_p99_vs_fake_quant"],
+                "err_vs_fp64": BAR * fq["logits_err_vs_fp64"],
+                "order_floor_max": fl["logits_max_vs_fake_quant"],
+                "order_floor_p99": fl["logits_p99_vs_fake_quant"]}
+        rep["criteria"] = crit
+        for name, r in rep.items():
+            if name in (ref_name, floor_name, "criteria", "seed") or not isinstance(r, dict):
+                continue
+            r["ratio_max_to_floor"] = r["logits_max_vs_fake_quant"] / crit["order_floor_max"]
+            r["ratio_p99_to_floor"] = r["logits_p99_vs_fake_quant"] / crit["order_floor_p99"]
+            if r["logits_max_vs_fake_quant"] > crit["max_vs_fake_quant"]:
+                failures.append((rep["seed"], name, "max", r["logits_max_vs_fake_quant"]))
+            if r["logits_p99_vs_fake_quant"] > crit["p99_vs_fake_quant"]:
+                failures.append((rep["seed"], name, "p99", r["logits_p99_vs_fake_quant"]))
+            if r["logits_err_vs_fp64"] > crit["err_vs_fp64"]:
+                failures.append((rep["seed"], name, "fp64", r["logits_err_vs_fp64"]))
+    doc = {"bar": f"<= {BAR} x order floor per seed", "seeds": reps, "failures": failures}
+    out = os.environ.get(out_env or "QLIN_PARITY_OUT")
     if out:
         with open(out, "w") as f:
-            json.dump(rep, f, indent=1)
-    print(json.dumps(rep))
-    assert fq < 1e-2, rep
-    for name in paths:
-        if name in (ref_name, floor_name):
-            continue
-        r = rep[name]
-        assert r["logits_err_vs_fp64"] <= rep["criteria"]["err_vs_fp64_max"], (name, rep)
-        assert r["logits_rel_vs_fake_quant"] <= rep["criteria"]["rel_vs_fake_quant_max"], (name, rep)
+            json.dump(doc, f, indent=1)
+    print(json.dumps(doc))
+    for rep in reps:
+        assert rep[ref_name]["logits_err_vs_fp64"] < 1e-2, rep
+    assert not failures, failures
 
 
-@torch.no_grad()
-def test_full_width_decode_three_way():
+def _decode_seed(seed):
     cfg = _cfg()
     dev = torch.device("cuda")
-    model = build_random_quant_llama(cfg, quant_args(4, 128), seed=21, device=dev,
+    model = build_random_quant_llama(cfg, quant_args(4, 128), seed=seed, device=dev,
                                      dtype=torch.float16)
     rtn_quantize_(model)  # fake-quant state: weight == W_dq, dense F.linear (the reference path)
-    g = torch.Generator(device=dev).manual_seed(3)
+    g = torch.Generator(device=dev).manual_seed(seed + 1)
     D = cfg.hidden_size // cfg.num_attention_heads
     past = [(torch.randn(1, cfg.num_key_value_heads, KV, D, device=dev, dtype=torch.float16,
                          generator=g),
@@ -167,8 +222,6 @@ def test_full_width_decode_three_way():
     h64 = x[0, 0].double()
     for layer, pkv in zip(model.layers, past):
         h64 = _ref64_decode(layer, h64, pkv, float(KV), cfg)
-    logits64 = _rms64(h64, model.norm.weight.double(), cfg.rms_norm_eps) @ \
-        model.lm_head.weight.double().T
 
     def run(kv_cache=False):
         h = x
@@ -178,7 +231,7 @@ def test_full_width_decode_three_way():
                 pkv = layer.self_attn.adopt_kv_cache(pkv)
             h = layer(h, attention_mask=mask, position_ids=pos, past_key_value=pkv,
                       use_cache=kv_cache)[0]
-        return h[0, 0], model.head(h)[0, 0]
+        return h[0, 0]
 
     paths = {"fake_quant": run()}
     _reorder_reference(model, True)
@@ -190,35 +243,27 @@ def test_full_width_decode_three_way():
     for layer in model.layers:
         layer.fuse_packed_projections(kv_cache=True)
     paths["fused_kv_cache"] = run(kv_cache=True)
-    from models.decode_engine import DecodeEngine
-    eng = DecodeEngine(model.layers)
-    if eng.reason is None:
-        views = [layer.self_attn.adopt_kv_cache(pkv) for layer, pkv in zip(model.layers, past)]
-        h, _ = eng.step(x, pos, views, mask)
-        assert eng.status() == 0
-        paths["decode_engine"] = (h[0, 0], model.head(h)[0, 0])
-
-    rep = {"layers": LAYERS, "kv_len": KV + 1,
-           "shapes": "LLaMA3-8B (4096 / 14336 / 32q 8kv / 128256), int4 g128, batch 1"}
-    for name, (h, lg) in paths.items():
-        rep[name] = {"logits_err_vs_fp64": _rel(lg, logits64), "hidden_err_vs_fp64": _rel(h, h64),
-                     "logits_rel_vs_fake_quant": _rel(lg, paths["fake_quant"][1]),
-                     "hidden_rel_vs_fake_quant": _rel(h, paths["fake_quant"][0])}
-    _judge(rep, paths)
+    _progress("decode seed", seed, "paths done")
+    rep = _report(seed, paths, model, cfg, h64)
+    rep.update(layers=LAYERS, kv_len=KV + 1,
+               shapes="LLaMA3-8B (4096 / 14336 / 32q 8kv / 128256), int4 g128, batch 1")
+    del model
+    torch.cuda.empty_cache()
+    return rep
 
 
 @torch.no_grad()
-def test_full_width_prefill_three_way():
-    """A 256-token causal window (positions 0..255) through the same four full-width layers:
-    fake-quant, its reordered twin, packed (MFMA GEMM), and packed + fused layer + the fused
-    prefill-attention kernel (opt-in mode, DESIGN.md §4 qlin_attn_prefill)."""
-    cfg = _cfg()
+def test_full_width_decode_three_way():
+    _judge([_decode_seed(s) for s in SEEDS])
+
+
+def _prefill_seed(seed, layers, S):
+    cfg = _cfg(layers)
     dev = torch.device("cuda")
-    S = 256
-    model = build_random_quant_llama(cfg, quant_args(4, 128), seed=22, device=dev,
+    model = build_random_quant_llama(cfg, quant_args(4, 128), seed=seed, device=dev,
                                      dtype=torch.float16)
     rtn_quantize_(model)
-    g = torch.Generator(device=dev).manual_seed(4)
+    g = torch.Generator(device=dev).manual_seed(seed + 1)
     x = torch.randn(1, S, cfg.hidden_size, device=dev, dtype=torch.float16, generator=g)
     mask = causal_mask(1, S, torch.float16, dev)
     pos = torch.arange(S, device=dev)[None]
@@ -226,14 +271,13 @@ def test_full_width_prefill_three_way():
     h64 = x[0].double()
     for layer in model.layers:
         h64 = _ref64_window(layer, h64, cfg)
-    logits64 = _rms64(h64, model.norm.weight.double(), cfg.rms_norm_eps) @ \
-        model.lm_head.weight.double().T
+    _progress("prefill seed", seed, "layers", layers, "fp64 done")
 
     def run():
         h = x
         for layer in model.layers:
             h = layer(h, attention_mask=mask, position_ids=pos)[0]
-        return h[0], model.head(h)[0]
+        return h[0]
 
     paths = {"fake_quant": run()}
     _reorder_reference(model, True)
@@ -243,12 +287,31 @@ def test_full_width_prefill_three_way():
         pack_quant_linears(layer)
     paths["packed"] = run()
     for layer in model.layers:
+        layer.fuse_packed_projections()
+    paths["fused"] = run()
+    for layer in model.layers:
         layer.fuse_packed_projections(prefill_attention=True)
     paths["fused_prefill_attention"] = run()
-    rep = {"layers": LAYERS, "window": S,
-           "shapes": "LLaMA3-8B (4096 / 14336 / 32q 8kv / 128256), int4 g128, causal window"}
-    for name, (h, lg) in paths.items():
-        rep[name] = {"logits_err_vs_fp64": _rel(lg, logits64), "hidden_err_vs_fp64": _rel(h, h64),
-                     "logits_rel_vs_fake_quant": _rel(lg, paths["fake_quant"][1]),
-                     "hidden_rel_vs_fake_quant": _rel(h, paths["fake_quant"][0])}
-    _judge(rep, paths)
+    _progress("prefill seed", seed, "paths done")
+    rep = _report(seed, paths, model, cfg, h64)
+    rep.update(layers=layers, window=S,
+               shapes="LLaMA3-8B (4096 / 14336 / 32q 8kv / 128256), int4 g128, causal window")
+    del model
+    torch.cuda.empty_cache()
+    return rep
+
+
+@torch.no_grad()
+def test_full_width_prefill_three_way():
+    """A 256-token causal window (positions 0..255) through four full-width layers: fake-quant,
+    its reordered twin, packed (MFMA GEMM), the fused layer, and the fused layer + the fused
+    prefill-attention kernel (opt-in mode, DESIGN.md §4 qlin_attn_prefill)."""
+    _judge([_prefill_seed(s, LAYERS, 256) for s in SEEDS], out_env="QLIN_PARITY_OUT_PREFILL")
+
+
+@torch.no_grad()
+def test_full_depth_prefill_attention_mode():
+    """The opt-in prefill-attention mode through all 32 LLaMA3-8B layers (a 128-token window):
+    amplified over 32 random layers, its distance to the fake-quant logits is held to the
+    reference's own order floor at the same depth."""
+    _judge([_prefill_seed(s, 32, 128) for s in SEEDS[:2]], out_env="QLIN_PARITY_OUT_PREFILL32")

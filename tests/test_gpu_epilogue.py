@@ -253,65 +253,3 @@ def test_rmsnorm_linear_rejects_unsupported():
     x2 = t(np.ones((2, 1024), np.float16))
     with pytest.raises(ValueError):
         qlin.rmsnorm_linear_ep(x2, w, 1e-5, qw, qsz, None, 256, 1024, 4, 128, fl)
-
-
-@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (1000 + 24, 512)])
-def test_residual_sumsq_partials(N, K):
-    """qlin_linear_res_sumsq_f16 (ABI 8): the same fp16 output as the residual epilogue, bit for
-    bit, plus one partial sum of squares per 16 outputs (the next RMSNorm's statistics) equal to
-    a float64 sum of the fp16 outputs' squares to fp32 rounding."""
-    qw, qsz, fl = _packed(N, K, 31)
-    rs = np.random.RandomState(N)
-    x = t(rs.randn(1, 1, K).astype(np.float16))
-    r = t((rs.randn(1, 1, N) * 4).astype(np.float16))
-    ref = qlin.linear_ep(x, qw, qsz, None, N, K, 4, 128, fl, epilogue=qlin.EP_RESIDUAL,
-                         residual=r)
-    sq = torch.full(((N + 15) // 16,), float("nan"), device="cuda")
-    got = qlin.linear_res_sumsq(x, qw, qsz, None, N, K, 4, 128, fl, r, sq)
-    assert torch.equal(got, ref)
-    y = got.double().reshape(-1)
-    y = torch.nn.functional.pad(y, (0, sq.numel() * 16 - N))
-    want = (y * y).reshape(-1, 16).sum(-1)
-    assert torch.allclose(sq.double(), want, rtol=1e-6, atol=0)
-
-
-@pytest.mark.parametrize("N,ep", [(6144, "none"), (28672, "silu")])
-def test_rmsnorm_linear_precomputed_statistics_and_rope_row(N, ep):
-    """qlin_rmsnorm_linear_ep_f16 with sumsq_in (the producer's partials) matches the in-kernel
-    statistics to an fp16 ulp of the normed x, and the rope gather copies the position's cos /
-    sin rows exactly; attn_decode_rope over the gathered rows (position_ids None) is bit-identical
-    to the call that looks the position up itself."""
-    K = 4096
-    qw, qsz, fl = _packed(N, K, 41)
-    rs = np.random.RandomState(N + 1)
-    xin = t(rs.randn(1, 1, K).astype(np.float16))
-    h = t(rs.randn(1, 1, K).astype(np.float16))
-    qw_o, qsz_o, fl_o = _packed(K, K, 42)
-    sq = torch.empty(K // 16, device="cuda")
-    x = qlin.linear_res_sumsq(xin, qw_o, qsz_o, None, K, K, 4, 128, fl_o, h, sq)
-    w = torch.tensor((1 + 0.1 * rs.randn(K)).astype(np.float32), device="cuda")
-    epc = qlin.EP_SILU_MUL if ep == "silu" else qlin.EP_NONE
-    ref = qlin.rmsnorm_linear_ep(x, w, 1e-5, qw, qsz, None, N, K, 4, 128, fl, epilogue=epc)
-    rows = 300
-    cos = torch.tensor(rs.randn(rows, 128).astype(np.float32), device="cuda")
-    sin = torch.tensor(rs.randn(rows, 128).astype(np.float32), device="cuda")
-    pos = torch.tensor([[123]], device="cuda")
-    out = torch.full((2, 128), float("nan"), device="cuda")
-    got = qlin.rmsnorm_linear_ep(x, w, 1e-5, qw, qsz, None, N, K, 4, 128, fl, epilogue=epc,
-                                 sumsq=sq, rope=(pos, cos, sin, out))
-    scale = ref.float().abs().max().item()
-    assert (got.float() - ref.float()).abs().max().item() <= 2e-3 * scale
-    assert (got == ref).float().mean().item() > 0.9
-    assert torch.equal(out[0], cos[123]) and torch.equal(out[1], sin[123])
-    # the attention launch over the gathered rows == the one that reads position_ids
-    Hq, Hkv, D, L0 = 32, 8, 128, 77
-    g = torch.Generator(device="cuda").manual_seed(7)
-    qkv = torch.randn(1, 1, (Hq + 2 * Hkv) * D, device="cuda", generator=g).half()
-    q, k, v = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
-    kc = torch.randn(1, Hkv, 256, D, device="cuda", generator=g).half()
-    vc = torch.randn(1, Hkv, 256, D, device="cuda", generator=g).half()
-    kc2, vc2 = kc.clone(), vc.clone()
-    a = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, L0, None, D ** 0.5)
-    b = qlin.attn_decode_rope(q, k, v, out[0:1], out[1:2], None, Hq, Hkv, D, kc2, vc2, L0, None,
-                              D ** 0.5)
-    assert torch.equal(a, b) and torch.equal(kc, kc2) and torch.equal(vc, vc2)

@@ -65,13 +65,12 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert ep(p, p, 0, p, None, None, p, 1, 16, 64, 4, 64, 0, 9, 0, None, 0, None) == 1  # act bits
     assert ep(p, p, 0, p, None, None, p, 100, 16, 64, 4, 64, 0, 8, 0, None, 0, None) == 1  # no ws
     assert ep(p, p, 0, p, None, None, p, 100, 16, 64, 4, 64, 0, 8, 0, p, 64, None) == 1  # short ws
-    # ABI 8: residual + statistics needs its partials buffer; precomputed statistics must be
-    # one partial per 16 features of x
-    assert lib.qlin_linear_res_sumsq_f16(p, p, 0, p, None, p, p, 16, 64, 4, 64, None, None) == 1
-    assert lib.qlin_rmsnorm_linear_ep_f16(p, p, 0, p, p, 1e-5, None, None, p, 1, 16, 128, 4, 128,
-                                          0, p, 3, None, None, None, 0, None, None) == 1
-    assert lib.qlin_rmsnorm_linear_ep_f16(p, p, 0, p, p, 1e-5, None, None, p, 1, 16, 128, 4, 128,
-                                          0, None, 0, None, None, None, 0, p, None) == 1  # rope
+    # ABI 10: the fused RMSNorm + linear takes one token row on whole k-tiles
+    assert lib.qlin_rmsnorm_linear_supported(1, 16, 256, 4, 128) == 1
+    assert lib.qlin_rmsnorm_linear_supported(2, 16, 256, 4, 128) == 0
+    assert lib.qlin_rmsnorm_linear_supported(1, 16, 1000, 4, 40) == 0
+    assert lib.qlin_rmsnorm_linear_ep_f16(p, p, 0, p, p, 1e-5, None, None, p, 1, 16, 256, 4, 128,
+                                          1, None) == 1  # residual epilogue without residual
     assert lib.qlin_pack_codes(None, 16, 64, 4, None, None) == 1
     assert lib.qlin_pack_codes(p, 16, 48, 4, p, None) == 1  # K % 32
     assert lib.qlin_pack_codes(p, 16, 64, 5, p, None) == 1  # bits
@@ -81,23 +80,8 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert gb(p, 256, p, 16, 0, p, 127, None, 0, p, 16, 2, 1, 16, 128, 4, 128, None) == 1  # x
     assert gb(p, 256, p, 16, 0, p, 128, p, 8, p, 16, 2, 1, 16, 128, 4, 128, None) == 1  # bias
     assert gb(p, 256, p, 16, 0, p, 128, None, 0, p, 16, 70000, 1, 16, 128, 4, 128, None) == 1
-    # ABI 9: the decode attention's split merge inside o_proj takes 2..10 splits, batch 1
     assert lib.qlin_attn_decode_splits(1, 8, 40) == 1 and lib.qlin_attn_decode_splits(1, 8, 0) == -1
-    assert 2 <= lib.qlin_attn_decode_splits(1, 8, 513) <= 10
-    assert lib.qlin_attn_merge_linear_supported(513, 32, 8, 4096, 4, 128, 0) == 1
-    assert lib.qlin_attn_merge_linear_supported(40, 32, 8, 4096, 4, 128, 0) == 0    # one split
-    assert lib.qlin_attn_merge_linear_supported(4096, 32, 8, 4096, 4, 128, 0) == 0  # > 10 splits
-    assert lib.qlin_attn_merge_linear_supported(513, 32, 8, 4096, 4, 128, 8) == 0   # wide zeros
-    assert lib.qlin_attn_merge_linear_supported(513, 32, 8, 4096, 5, 128, 0) == 0   # bits
-    ml = lib.qlin_attn_merge_linear_f16
-    assert ml(None, 513, 32, 8, p, p, 0, None, p, p, 4096, 4, 128, None) == 1  # partials
-    assert ml(p, 513, 32, 8, p, p, 0, None, None, p, 4096, 4, 128, None) == 1  # residual
-    assert ml(p, 40, 32, 8, p, p, 0, None, p, p, 4096, 4, 128, None) == 1      # one split
-    assert lib.qlin_prefetch(None, 64, 0, None) == 1 and lib.qlin_prefetch(p, -1, 0, None) == 1
-    assert lib.qlin_prefetch(ctypes.c_void_p(8), 64, 0, None) == 1  # not 16-B aligned
-    pf = lib.qlin_attn_decode_rope_pf
-    assert pf(None, 0, None, 0, None, 0, None, None, 0, None, 0, None, None, 0, None, None, 0,
-              1, 32, 8, 513, 128, 11.3, None, None, None, p, 64, 0) == 1  # no blocks
+    assert lib.qlin_attn_decode_splits(1, 8, 513) >= 2
     assert lib.qlin_gemm_block_cols(0, 16, 4) == -1 and lib.qlin_gemm_block_cols(16, 16, 5) == -1
     assert lib.qlin_error_string(1) == b"invalid argument"
 

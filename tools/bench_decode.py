@@ -94,35 +94,6 @@ def main():
         past[i] = layer.self_attn.adopt_kv_cache(past[i])
     cache["use"] = True
     res["packed_fused_kv_cache_us"], y_kv = timed()
-    # + the persistent decode engine: the whole stack in ONE launch per token
-    from models.decode_engine import DecodeEngine
-    eng = DecodeEngine(st.layers)
-    res["engine_reason"] = eng.reason
-    if eng.reason is None:
-        for i, layer in enumerate(st.layers):
-            past[i] = layer.self_attn.adopt_kv_cache(past[i])
-        pos1 = pos.clone()
-
-        def eng_step():
-            return eng.step(x, pos1, past, mask)[0]
-        with torch.no_grad():
-            y_en = eng_step()
-            torch.cuda.synchronize()
-            res["engine_status"] = eng.status()
-            for _ in range(3):
-                eng_step()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
-            e0.record()
-            for _ in range(a.reps):
-                eng_step()
-            e1.record()
-            torch.cuda.synchronize()
-        res["engine_us"] = e0.elapsed_time(e1) * 1e3 / a.reps / a.layers
-        res["rel_err_engine_vs_fused"] = float((y_en.float() - y_kv.float()).abs().max()
-                                               / y_kv.float().abs().max())
-        res["rel_err_engine_vs_fake_quant"] = float((y_en.float() - y_fq.float()).abs().max()
-                                                    / y_fq.float().abs().max())
     params = sum(m.in_features * m.out_features for l in st.layers for m in l.modules()
                  if hasattr(m, "qweight") and m.__class__.__name__ == "QuantLinear") / a.layers
     wbytes = params * 0.5 + params / 128 * 3
@@ -141,9 +112,6 @@ def main():
            "kv_cache_equal_to_cat": bool(torch.equal(y_kv, y_fu)),
            "est_32_layer_token_ms": round(res["packed_fused_us"] * 32 / 1e3, 3),
            "est_32_layer_token_ms_kv_cache": round(res["packed_fused_kv_cache_us"] * 32 / 1e3, 3)}
-    if "engine_us" in res:
-        out["engine_weight_GBps"] = round(wbytes / res["engine_us"] / 1e3, 1)
-        out["engine_frac_of_8TBps"] = round(wbytes / res["engine_us"] / 1e3 / 8000, 4)
     print(json.dumps(out))
 
 
