@@ -108,71 +108,100 @@ def parse():
     return ap.parse_args()
 
 
+def _host_cpus():
+    """(CPUs this process may run on, physical cores among them, CPU model) from the affinity
+    mask and /proc/cpuinfo (SMT siblings share a (physical id, core id) pair)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = list(range(os.cpu_count() or 1))
+    model, cores, cur = None, set(), {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f.read().split("\n") + [""]:
+                if not line.strip():
+                    if cur.get("processor") in cpus:
+                        cores.add((cur.get("physical id", 0), cur.get("core id", cur["processor"])))
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k in ("processor", "physical id", "core id"):
+                    cur[k] = int(v)
+                elif k == "model name" and model is None:
+                    model = v
+    except OSError:
+        pass
+    return cpus, (len(cores) or len(cpus)), model
+
+
 def cpu_baseline(M, N, K, bits, group, seconds):
     """The reference's fake-quant path on the host cores, restated in torch
-    (oracle/torch_ref.py, pinned bit-exactly to the reference's golden W_dq), with
-    torch.set_num_threads(<CPUs this process may run on>):
+    (oracle/torch_ref.py, pinned bit-exactly to the reference's golden W_dq), swept over torch
+    thread counts {1, 8, 16, 32, 64, 128, all} and dtypes {fp16, fp32}:
       mode (ii) — what the reference runs at eval (weight == W_dq; quant/int_linear.py:62):
-               fp16 F.linear(x, W_dq) over a bounded sample of distinct pre-dequantized matrices;
-               value = median TFLOP/s of 5 timed runs after a warm-up;
+               F.linear(x, W_dq) over a bounded sample of distinct pre-dequantized matrices;
+               TFLOP/s of the best of 3 timed runs per (threads, dtype);
       mode (i)  — quantize every call (use_weight_quant=True, quant/quantizer.py:118-159 then
-               F.linear): median ms per call of >= 5 calls."""
+               F.linear, fp16): median ms per call, per thread count.
+    value = the reference's op as it runs (fp16 F.linear) at its best thread count."""
     import statistics
     import torch
     import torch.nn.functional as F
     from oracle import torch_ref as TR
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        threads = os.cpu_count() or 1
+    cpus, phys, model = _host_cpus()
+    avail = len(cpus)
+    counts = sorted({t for t in (1, 8, 16, 32, 64, 128) if t <= avail} | {avail})
     prev = torch.get_num_threads()
-    torch.set_num_threads(threads)
+    sweep, qsweep = {}, {}
+    nmat = 4
+    g = torch.Generator().manual_seed(0)
+    w16 = [(torch.randn(N, K, generator=g) * 0.02).half() for _ in range(nmat)]
+    wdq16 = [TR.quantize(w, bits, group)[0].contiguous() for w in w16]
+    wdq32 = [w.float() for w in wdq16]
+    x16 = torch.randn(M, K, generator=g).half()
+    x32 = x16.float()
+    per_run = max(0.05, 0.5 * seconds / (len(counts) * 2 * 3))
     try:
-        g = torch.Generator().manual_seed(0)
-        nmat = 4
-        w16 = [(torch.randn(N, K, generator=g) * 0.02).half() for _ in range(nmat)]
-        wdq = [TR.quantize(w, bits, group)[0].contiguous() for w in w16]
-        x = torch.randn(M, K, generator=g).half()
-        F.linear(x, wdq[0])  # warm-up
-        runs, products = [], 0
-        per_run = max(0.2, 0.6 * seconds / 5)
-        for _ in range(5):
-            n = 0
-            t0 = time.perf_counter()
-            while time.perf_counter() - t0 < per_run:
-                for w in wdq:
-                    F.linear(x, w)
-                    n += 1
-            dt = time.perf_counter() - t0
-            runs.append(2.0 * M * N * K * n / dt / 1e12)
-            products += n
-        calls = []
-        t1 = time.perf_counter()
-        while len(calls) < 5 or (time.perf_counter() - t1 < 0.3 * seconds and len(calls) < 50):
-            t0 = time.perf_counter()
-            TR.quant_linear(x, w16[len(calls) % nmat], bits, group)
-            calls.append(time.perf_counter() - t0)
+        for t in counts:
+            torch.set_num_threads(t)
+            for dt, x, ws in (("fp16", x16, wdq16), ("fp32", x32, wdq32)):
+                F.linear(x, ws[0])  # warm-up
+                best = 0.0
+                for _ in range(3):
+                    n = 0
+                    t0 = time.perf_counter()
+                    while time.perf_counter() - t0 < per_run:
+                        for w in ws:
+                            F.linear(x, w)
+                            n += 1
+                    best = max(best, 2.0 * M * N * K * n / (time.perf_counter() - t0) / 1e12)
+                sweep[f"{dt}@{t}"] = round(best, 6)
+        for t in sorted({1, min(8, avail), avail}):
+            torch.set_num_threads(t)
+            calls = []
+            t1 = time.perf_counter()
+            while len(calls) < 3 or (time.perf_counter() - t1 < 0.4 * seconds / 3 and len(calls) < 20):
+                t0 = time.perf_counter()
+                TR.quant_linear(x16, w16[len(calls) % nmat], bits, group)
+                calls.append(time.perf_counter() - t0)
+                if time.perf_counter() - t1 > 0.4 * seconds:
+                    break
+            qsweep[f"fp16@{t}"] = round(statistics.median(calls) * 1e3, 2)
     finally:
         torch.set_num_threads(prev)
-    cpu_model = None
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": round(statistics.median(runs), 6), "unit": "TFLOP/s", "cores": int(threads),
-            "kind": "port", "cpu_model": cpu_model, "nproc": os.cpu_count(),
-            "runs_tflops": [round(r, 6) for r in runs],
-            "sample": (f"torch fp16 F.linear(x, W_dq) on the host (the reference's eval op, "
+    best_key = max((k for k in sweep if k.startswith("fp16@")), key=lambda k: sweep[k])
+    best_t = int(best_key.split("@")[1])
+    return {"value": sweep[best_key], "unit": "TFLOP/s", "cores": best_t,
+            "kind": "port", "cpu_model": model, "physical_cores": phys,
+            "cpus_available": avail, "nproc": os.cpu_count(),
+            "sweep_tflops": sweep, "quantize_every_call_ms": qsweep,
+            "sample": (f"torch F.linear(x, W_dq) on the host (the reference's eval op, "
                        f"quant/int_linear.py:62; W_dq from oracle/torch_ref.py), M={M} N={N} "
                        f"K={K}, {nmat} distinct pre-dequantized int{bits} g{group} matrices, "
-                       f"5 runs of {per_run:.1f}s ({products} products), median; "
-                       f"torch.set_num_threads({threads}) = the CPUs this process may use"),
-            "quantize_every_call_ms": round(statistics.median(calls) * 1e3, 2),
-            "quantize_every_call_calls": len(calls)}
+                       f"best of 3 runs of {per_run:.2f}s per (dtype, threads); value = fp16 at "
+                       f"its best thread count ({best_t} of {avail} CPUs available, {phys} "
+                       f"physical cores); quantize_every_call_ms: use_weight_quant=True, fp16")}
 
 
 def decode_layer_bytes(cfg, L, bits=4, group=128):

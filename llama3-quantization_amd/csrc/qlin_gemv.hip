@@ -366,15 +366,24 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
 // (scale, zero) words; the x wait does not wait for the weights.
 // ---------------------------------------------------------------------------------------------
 #ifndef GEMV_ROWS_BPC  // dev knob: resident blocks per CU of a persistent (multi-row) launch
-#define GEMV_ROWS_BPC 1
+#define GEMV_ROWS_BPC 2
 #endif
-#ifndef GEMV_ROWS_CONTIG  // dev knob: 1 = wave w takes k-tiles w*TPW .. (w+1)*TPW - 1,
-#define GEMV_ROWS_CONTIG 0  // 0 = k-tiles w, w + W, w + 2W, ... (same arithmetic, other addresses)
-#endif
+#ifndef GEMV_ROWS_CONTIG  // dev knob: 1 = wave w takes k-tiles w*TPW .. (w+1)*TPW - 1, 0 = k-tiles
+#define GEMV_ROWS_CONTIG 2  // w, w + W, w + 2W, ...; 2 = contiguous for TPW = 8 only (measured:
+#endif                      // down 8.25 vs 8.39 us contiguous, 4096^2 3.86 vs 4.02 strided)
 #ifndef GEMV_ROWS_MAXPF  // dev knob: most tiles in flight per wave
 #define GEMV_ROWS_MAXPF 8
 #endif
-constexpr int kRowsMaxTPW = 8;  // k-tiles per wave and row: x words held in registers at start
+#ifndef GEMV_ROWS_SZFIRST  // dev knob: 1 = each tile's (scale, zero) words issued before its codes,
+#define GEMV_ROWS_SZFIRST 0  // tile by tile (scheduling barriers keep the order)
+#endif
+#ifndef GEMV_ROWS_SYNC  // dev knob: 1 = __syncthreads() at the row barrier (drains vmcnt)
+#define GEMV_ROWS_SYNC 0
+#endif
+#ifndef GEMV_ROWS_LDS_MIN  // dev knob: dynamic LDS bytes asked of a persistent launch at least
+#define GEMV_ROWS_LDS_MIN 0  // (more than half of the CU's 160 KB admits one block per CU)
+#endif
+constexpr int kRowsMaxTPW = 8;  // k-tiles per wave and row
 
 struct RowsArgs {
   const uint32_t* qw;   // tile row 0 of qweight
@@ -383,103 +392,114 @@ struct RowsArgs {
   const _Float16* bias;
   const _Float16* res;  // kEpResidual
   _Float16* y;
-  const float* nw;      // nrm: RMSNorm weight, fp32 [K]
+  const float* nw;      // NRM: RMSNorm weight, fp32 [K]
   float eps;
-  int ep, nrm;
-  int N, K, Kt, G, Nt;
-  int W, TPW;           // waves per block, k-tiles per wave and row (W * TPW == Kt)
-  int nb;               // blocks of the grid: block b owns tile rows b, b + nb, ...
-  int kt0m, kts;        // wave w's k-tile i = w * kt0m + i * kts
+  int ep, has_bias;     // bias / res always readable (the host points absent ones at y)
+  int64_t nres;         // readable elements at res
+  int N, K, Kt, G;
+  int W;                // waves per block (W * TPW == Kt)
+  int nb, rpb, extra;   // blocks; block b owns rpb + (b < extra) tile rows b, b + nb, ...
+  int64_t wstep, sstep; // qweight / qsz words between two rows of a block (nb tile rows)
   uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
+#ifdef GEMV_ROWS_STAMP  // dev build only: per-wave s_memrealtime stamps [block][wave][8]
+  uint64_t* stamps;
+#endif
 };
+#ifdef GEMV_ROWS_STAMP
+#define ROWS_STAMP(k)                                                                      \
+  if (a.stamps && lane == 0)                                                               \
+    a.stamps[((int64_t)blockIdx.x * kMaxWaves + wave) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+inline uint64_t* g_rows_stamps = nullptr;  // set by qlin_dev_rows_stamps (dev build)
+#else
+#define ROWS_STAMP(k)
+#endif
 
-template <int BITS, int GPT, int ZM, int PF>
+template <int BITS, int GPT, int ZM, int TPW, int PF, bool NRM>
 __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t xs_dyn[];  // [W][TPW][64] x words
-  __shared__ __attribute__((aligned(16))) float red[2][kTileN][kMaxWaves];  // row partials
-  __shared__ float nss[kMaxWaves];                                          // nrm: sums of squares
+  __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][TPW * 64];  // the wave's x words
+  __shared__ __attribute__((aligned(16))) float red[2][kTileN][kMaxWaves];   // row partials
+  __shared__ float nss[NRM ? kMaxWaves : 1];                                 // sums of squares
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
   const int b = blockIdx.x;
-  const int TPW = a.TPW;
-  const int nrows = (a.Nt - 1 - b) / a.nb + 1;  // >= 1
-  const int T = nrows * TPW;                    // tiles this wave streams (host: T >= PF)
-  const int kt0 = wave * a.kt0m;
-  uint32_t* xsl = xs_dyn + wave * TPW * 64;
-  const int64_t wrow = (int64_t)a.Kt * (64 * BITS);  // qweight words per tile row
-  const int64_t srow = (int64_t)a.G * kTileN;          // qsz words per tile row
+  ROWS_STAMP(0);
+  const int nrows = a.rpb + (b < a.extra ? 1 : 0);
+  const int T = nrows * TPW;  // tiles this wave streams (host: T >= PF)
+  constexpr bool kContig = GEMV_ROWS_CONTIG == 2 ? TPW >= 8 : GEMV_ROWS_CONTIG != 0;
+  const int kt0 = kContig ? wave * TPW : wave;
+  const int kts = kContig ? 1 : a.W;
   auto group_of_tile = [&](int kt) {
     return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
   };
 
   // x words of this wave's k-tiles (lane l: k = 128 kt + 2l, 2l + 1), the same for every row;
-  // slots past TPW repeat the last tile (L1 hits, never used)
-  uint32_t xw[kRowsMaxTPW];
-  float2 nwv[kRowsMaxTPW];
+  // issued first (in-order completion: their wait does not wait for the weights)
+  const _Float16* xp = a.x + kt0 * kTileK + 2 * lane;
+  uint32_t xw[TPW];
+  float2 nwv[NRM ? TPW : 1];
 #pragma unroll
-  for (int i = 0; i < kRowsMaxTPW; ++i) {
-    const int kt = kt0 + min(i, TPW - 1) * a.kts;
-    xw[i] = *reinterpret_cast<const uint32_t*>(a.x + kt * kTileK + 2 * lane);
-  }
-  if (a.nrm) {  // block-uniform
+  for (int i = 0; i < TPW; ++i) xw[i] = *reinterpret_cast<const uint32_t*>(xp + i * kts * kTileK);
+  if constexpr (NRM) {
+    const float* np = a.nw + kt0 * kTileK + 2 * lane;
 #pragma unroll
-    for (int i = 0; i < kRowsMaxTPW; ++i) {
-      const int kt = kt0 + min(i, TPW - 1) * a.kts;
-      nwv[i] = *reinterpret_cast<const float2*>(a.nw + kt * kTileK + 2 * lane);
-    }
+    for (int i = 0; i < TPW; ++i) nwv[i] = *reinterpret_cast<const float2*>(np + i * kts * kTileK);
   }
 
-  // weight stream: the load cursor (row jl, k-tile il) runs PF tiles ahead of the compute cursor
+  // the epilogue operands of the first row this wave finishes (the epilogue of a block's j-th row
+  // runs on wave j % W: wave w's first is row w): loaded unconditionally (the host points absent
+  // operands at a readable buffer, never used) ahead of the weights, so no tile waits for them
+  const int NO = a.ep == kEpSiluMul ? 8 : kTileN;  // outputs per row
+  const int on = min(lane, NO - 1);
+  _Float16 ob0, ob1, ores;
+  auto load_epi = [&](int j) {
+    const int64_t row = (int64_t)(b + min(j, nrows - 1) * a.nb) * kTileN + on;
+    const int64_t nb_ = a.has_bias ? (int64_t)a.N : a.nres;  // readable bias elements
+    ob0 = a.bias[min(row, nb_ - 1)];
+    ob1 = a.bias[min(row + 8, nb_ - 1)];
+    ores = a.res[min(row, a.nres - 1)];
+  };
+  load_epi(wave);
+
+  // weight stream: the load cursor (row offset lq / ls, k-tile il) runs PF tiles ahead
   WTile<BITS, GPT> wt[PF];
+  const uint32_t* qwp = a.qw + ((int64_t)b * a.Kt + kt0) * (64 * BITS) + lane * BITS;
+  const uint32_t* szp = a.qsz + (int64_t)b * a.G * kTileN + n_in;
   int il = 0;
-  int64_t lq = (int64_t)b * wrow, ls = (int64_t)b * srow;  // the load row's qweight / qsz offsets
+  int64_t lq = 0, ls = 0;
   auto load = [&](int u) {
-    const int kt = kt0 + il * a.kts;
-    wt[u].pc = load_piece_nt<BITS>(a.qw + lq + kt * (64 * BITS) + lane * BITS);
-    const int g0 = group_of_tile(kt);
+    const int ki = il * kts;  // k-tile offset from kt0
+    const int g0 = group_of_tile(kt0 + ki);
+    if (GEMV_ROWS_SZFIRST) {
 #pragma unroll
-    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = a.qsz[ls + (g0 + s) * kTileN + n_in];
+      for (int s = 0; s < GPT; ++s) wt[u].sz[s] = szp[ls + (g0 + s) * kTileN];
+      wt[u].pc = load_piece_nt<BITS>(qwp + lq + ki * (64 * BITS));
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      wt[u].pc = load_piece_nt<BITS>(qwp + lq + ki * (64 * BITS));
+#pragma unroll
+      for (int s = 0; s < GPT; ++s) wt[u].sz[s] = szp[ls + (g0 + s) * kTileN];
+    }
     if (++il == TPW) {
       il = 0;
-      lq += (int64_t)a.nb * wrow;
-      ls += (int64_t)a.nb * srow;
+      lq += a.wstep;
+      ls += a.sstep;
     }
   };
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u);
 
-  // the epilogue operands of the first row this wave finishes (row j = wave: the epilogue of row j
-  // runs on wave j % W), fetched while the weights stream
-  const int NO = a.ep == kEpSiluMul ? 8 : kTileN;  // outputs per row
-  const int on = min(lane, NO - 1);
-  _Float16 ob0 = 0, ob1 = 0, ores = 0;
-  auto load_epi = [&](int j) {
-    const int64_t row = (int64_t)(b + min(j, nrows - 1) * a.nb) * kTileN + on;
-    const int64_t rc = min(row, (int64_t)a.N - 1);
-    if (a.bias) {
-      ob0 = a.bias[rc];
-      ob1 = a.bias[min(row + 8, (int64_t)a.N - 1)];
-    }
-    if (a.ep == kEpResidual) ores = a.res[rc];
-  };
-  load_epi(wave);
+  ROWS_STAMP(1);
 
-  if (wave == 0 && lane < kTileN) {  // partial columns of absent waves read as zero
-    for (int w = a.W; w < kMaxWaves; ++w) red[0][lane][w] = red[1][lane][w] = 0.f;
-  }
-
-  if (a.nrm) {
+  if constexpr (NRM) {
 #pragma clang fp contract(off)
     float ss = 0.f;
 #pragma unroll
-    for (int i = 0; i < kRowsMaxTPW; ++i) {
-      if (i < TPW) {
-        const h2 v = as_h2(xw[i]);
-        const float f0 = (float)v.x, f1 = (float)v.y;
-        ss = ss + f0 * f0;
-        ss = ss + f1 * f1;
-      }
+    for (int i = 0; i < TPW; ++i) {
+      const h2 v = as_h2(xw[i]);
+      const float f0 = (float)v.x, f1 = (float)v.y;
+      ss = ss + f0 * f0;
+      ss = ss + f1 * f1;
     }
     ss = wave_sum(ss);
     if (lane == 0) nss[wave] = ss;
@@ -489,16 +509,17 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
     for (int w = 0; w < a.W; ++w) tot += nss[w];
     const float rn = rsqrtf(tot / (float)a.K + a.eps);
 #pragma unroll
-    for (int i = 0; i < kRowsMaxTPW; ++i) {
+    for (int i = 0; i < TPW; ++i) {
       const h2 v = as_h2(xw[i]);
       const float n0 = nwv[i].x * ((float)v.x * rn);
       const float n1 = nwv[i].y * ((float)v.y * rn);
       xw[i] = as_u32(h2{(_Float16)n0, (_Float16)n1});
     }
   }
+  uint32_t* xsl = &xs[wave][0];
 #pragma unroll
-  for (int i = 0; i < kRowsMaxTPW; ++i)
-    if (i < TPW) xsl[i * 64 + lane] = xw[i];
+  for (int i = 0; i < TPW; ++i) xsl[i * 64 + lane] = xw[i];
+  ROWS_STAMP(2);
 
   const Magics mg = make_magics<BITS>();
   f4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -506,14 +527,20 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
   auto epilogue = [&]() {
     if (lane < kTileN) red[par][lane][wave] = acc[0];
     acc = f4{0.f, 0.f, 0.f, 0.f};
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (GEMV_ROWS_SYNC) __syncthreads();
+    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (wave == ew) {  // wave-uniform
       const int64_t r = (int64_t)b + (int64_t)jc * a.nb;
-      auto total = [&](int n, _Float16 bv) {
+      auto total = [&](int n, _Float16 bv) {  // the W partials in a fixed tree order
         const f4* p = reinterpret_cast<const f4*>(&red[par][n][0]);
-        const f4 e = (p[0] + p[1]) + (p[2] + p[3]);
-        float t = (e[0] + e[1]) + (e[2] + e[3]);
-        if (a.bias) t += (float)bv;
+        f4 q[4] = {p[0], p[1], p[2], p[3]};
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) q[c][e] = 4 * c + e < a.W ? q[c][e] : 0.f;  // absent waves
+        const f4 e4 = (q[0] + q[1]) + (q[2] + q[3]);
+        float t = (e4[0] + e4[1]) + (e4[2] + e4[3]);
+        if (a.has_bias) t += (float)bv;
         return (float)(_Float16)t;  // F.linear's fp16 output
       };
       if (lane < NO) {
@@ -526,7 +553,7 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
           a.y[r * kTileN + lane] = (_Float16)t;
         }
       }
-      load_epi(jc + a.W);  // this wave's next epilogue row
+      if (jc + a.W < nrows) load_epi(jc + a.W);  // this wave's next epilogue row (multi-row)
     }
     if (++ew == a.W) ew = 0;
     par ^= 1;
@@ -548,7 +575,13 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
     step(std::integral_constant<int, 1>{});
     step(std::integral_constant<int, 2>{});
     step(std::integral_constant<int, 3>{});
+#ifdef GEMV_ROWS_STAMP
+    if (jc == 0 && ic == 0) ROWS_STAMP(3);  // the first tile computed
+#endif
     if (++ic == TPW) {  // block-uniform: the row is complete in every wave
+#ifdef GEMV_ROWS_STAMP
+      if (jc + 1 == nrows) ROWS_STAMP(4);  // the last tile computed
+#endif
       epilogue();
       ic = 0;
       ++jc;
@@ -573,14 +606,217 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
 #pragma unroll
   for (int u = 0; u < PF; ++u)
     if (u < rem) compute(u);
+  ROWS_STAMP(5);
 }
 
 // ---------------------------------------------------------------------------------------------
-// Decode fast path for 2..4 token rows: M <= 4, K % 128 == 0, group % 128 == 0 or group in
-// {32, 64}, no activation fake-quant.  Same arithmetic as gemv_kernel (exact W_dq, one MFMA per
-// k-step), built for the few microseconds a decode launch lasts (tools/dev/gemv_lab2.hip,
-// gemv_lab3.hip): block = one tile row, W waves split K (k-tiles w, w + W, ...),
-// every size-derived value precomputed on the host, all of a wave's tiles loaded up front.
+// Decode path for wide matrices (one token row, N >= 16 tile rows per CU): the "whole-row" kernel.
+//
+// The rows kernel splits every tile row's K over the W waves of a block, so each row ends in a
+// block barrier; over many rows those barriers lock the waves together and a row costs the
+// slowest wave's latency.  For wide matrices (gate/up: 1,792 tile rows) there are enough rows to
+// give every wave whole rows instead, as the batched streaming kernel does: wave w streams all K
+// of its tile row(s) with PF tiles in flight, one MFMA chain per row in k order (bit-identical
+// to qlin_gemm_f16 without split-K), and applies the epilogue itself (the gate / up halves of an
+// interleaved row tile meet by a lane shuffle).  The block's waves share x: it is staged once per
+// block in LDS (16-B chunks read by all threads; with the RMSNorm, normalised there at the
+// reference's rounding point after one block reduction of the sum of squares), and every A
+// fragment is a broadcast ds_read_b128 of it.  No barrier after the staging.
+// ---------------------------------------------------------------------------------------------
+constexpr int kWrowMaxWaves = 8;
+constexpr int kWrowXIter = 4;  // 16-B x chunks per thread (host: K <= 8 * 64 * waves * kWrowXIter)
+
+struct WrowArgs {
+  const uint32_t* qw;
+  const uint32_t* qsz;
+  const _Float16* x;
+  const _Float16* bias;
+  const _Float16* res;
+  _Float16* y;
+  const float* nw;      // NRM: RMSNorm weight fp32 [K]
+  float eps;
+  int ep, has_bias;     // bias / res always readable (the host points absent ones at y)
+  int64_t nres;         // readable elements at res
+  int N, K, Kt, G, Nt;
+  int nwaves;           // waves of the grid: wave g owns tile rows g, g + nwaves, ...
+  uint32_t cmagic;
+};
+
+template <int BITS, int GPT, int ZM, int PF, bool NRM>
+__global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const WrowArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 xs4[];  // x (normed), fp16 [K]: K / 8 chunks
+  __shared__ float nss[kWrowMaxWaves];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, n_in = lane & 15, q = lane >> 4;
+  const int nthr = blockDim.x;
+  const int gw = blockIdx.x * (nthr >> 6) + wave;  // this wave's grid index
+  const int nrow = gw < a.Nt ? (a.Nt - 1 - gw) / a.nwaves + 1 : 0;  // rows of this wave
+  auto group_of_tile = [&](int kt) {
+    return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
+  };
+
+  // x chunks of this thread (clamped: repeats are never stored), issued first
+  const int nch = a.K >> 3;
+  uint4 xc[kWrowXIter];
+  float4 nc[NRM ? 2 * kWrowXIter : 1];
+#pragma unroll
+  for (int i = 0; i < kWrowXIter; ++i) {
+    const int c = min(tid + i * nthr, nch - 1);
+    xc[i] = reinterpret_cast<const uint4*>(a.x)[c];
+    if constexpr (NRM) {
+      nc[2 * i] = reinterpret_cast<const float4*>(a.nw)[2 * c];
+      nc[2 * i + 1] = reinterpret_cast<const float4*>(a.nw)[2 * c + 1];
+    }
+  }
+
+  // the first PF tiles of the wave's first row (rows of PF-tile rounds: Kt % PF == 0)
+  WTile<BITS, GPT> wt[PF];
+  const int64_t wrow = (int64_t)a.Kt * (64 * BITS), srow = (int64_t)a.G * kTileN;
+  int64_t lr = gw;  // load cursor: row, k-tile
+  int lkt = 0;
+  const uint32_t* lqw = a.qw + lr * wrow + lane * BITS;
+  const uint32_t* lsz = a.qsz + lr * srow + n_in;
+  auto load = [&](int u) {
+    const int kt = lkt + u;
+    wt[u].pc = load_piece_nt<BITS>(lqw + kt * (64 * BITS));
+    const int g0 = group_of_tile(kt);
+#pragma unroll
+    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = lsz[(g0 + s) * kTileN];
+  };
+  if (nrow > 0) {  // wave-uniform
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load(u);
+  }
+
+  // stage x (normed) in LDS: one block reduction for the statistics, one barrier
+  if constexpr (NRM) {
+#pragma clang fp contract(off)
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < kWrowXIter; ++i) {
+      const h8 v = __builtin_bit_cast(h8, xc[i]);
+      float s8 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s8 = s8 + (float)v[j] * (float)v[j];
+      ss = ss + (tid + i * nthr < nch ? s8 : 0.f);
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) nss[wave] = ss;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float tot = 0.f;
+    for (int w = 0; w < (nthr >> 6); ++w) tot += nss[w];
+    const float rn = rsqrtf(tot / (float)a.K + a.eps);
+#pragma unroll
+    for (int i = 0; i < kWrowXIter; ++i) {
+      const h8 v = __builtin_bit_cast(h8, xc[i]);
+      const float w8[8] = {nc[2 * i].x, nc[2 * i].y, nc[2 * i].z, nc[2 * i].w,
+                           nc[2 * i + 1].x, nc[2 * i + 1].y, nc[2 * i + 1].z, nc[2 * i + 1].w};
+      h8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (_Float16)(w8[j] * ((float)v[j] * rn));
+      xc[i] = __builtin_bit_cast(uint4, o);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kWrowXIter; ++i)
+    if (tid + i * nthr < nch) xs4[tid + i * nthr] = xc[i];
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (nrow == 0) return;  // wave-uniform; no barrier below
+
+  const Magics mg = make_magics<BITS>();
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  int64_t cr = gw;  // compute cursor: row, k-tile
+  int ckt = 0;
+  const int NO = a.ep == kEpSiluMul ? 8 : kTileN;
+  _Float16 ob0 = 0, ob1 = 0, ores = 0;
+  auto load_epi = [&](int64_t r) {  // the row's epilogue operands, early in its stream
+    // unconditional (absent operands point at y, never used): no wait at a branch join
+    const int64_t row = r * kTileN + min(n_in, NO - 1);
+    const int64_t nb_ = a.has_bias ? (int64_t)a.N : a.nres;  // readable bias elements
+    ob0 = a.bias[min(row, nb_ - 1)];
+    ob1 = a.bias[min(row + 8, nb_ - 1)];
+    ores = a.res[min(row, a.nres - 1)];
+  };
+  load_epi(cr);
+  auto compute = [&](int u) {
+    const int kt = ckt + u;
+    h8 xa[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, xs4[kt * 16 + 4 * s + q]);
+    auto step = [&](auto S_) {
+      constexpr int S = decltype(S_)::value;
+      uint32_t v[4];
+      const GroupQ gq = make_group_w<BITS, ZM>(wt[u].sz[S * GPT / 4]);
+      dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
+      const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+  };
+  auto store = [&]() {  // C row 0 = acc[0] of lanes 0..15 (column n = lane)
+    float t = acc[0];
+    if (a.has_bias) t += (float)ob0;
+    t = (float)(_Float16)t;  // F.linear's fp16 output
+    const float up = __shfl(t, lane + 8);  // interleaved gate / up halves: lane n + 8 = up row n
+    if (a.ep == kEpSiluMul) {
+      if (lane < 8 && cr * kTileN + lane + 8 < a.N)
+        a.y[cr * 8 + lane] = (_Float16)(silu_rn16(t) * up);
+    } else if (lane < kTileN && cr * kTileN + lane < a.N) {
+      if (a.ep == kEpResidual) t += (float)ores;
+      a.y[cr * kTileN + lane] = (_Float16)t;
+    }
+    acc = f4{0.f, 0.f, 0.f, 0.f};
+  };
+  const int64_t rounds = (int64_t)nrow * (a.Kt / PF);
+  for (int64_t rd = 0; rd + 1 < rounds; ++rd) {
+    lkt += PF;
+    if (lkt == a.Kt) {  // wave-uniform: the load cursor moves to the wave's next row
+      lkt = 0;
+      lr += a.nwaves;
+      lqw = a.qw + lr * wrow + lane * BITS;
+      lsz = a.qsz + lr * srow + n_in;
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      compute(u);
+      load(u);
+    }
+    ckt += PF;
+    if (ckt == a.Kt) {  // wave-uniform: the row is complete
+      store();
+      ckt = 0;
+      cr += a.nwaves;
+      load_epi(cr);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u) compute(u);
+  store();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode fast path: M <= 4, K % 128 == 0, group % 128 == 0 or group in {32, 64}, no activation
+// fake-quant, at most 4 k-tiles per wave.  Same arithmetic as gemv_kernel (exact W_dq, one MFMA
+// per k-step), built for the few microseconds a decode launch lasts (tools/dev/gemv_lab2.hip,
+// gemv_lab3.hip):
+//   - everything the general kernel derives by integer division (tiles, groups, strides) comes
+//     precomputed from the host, so the first weight load issues a few scalar ops after the
+//     kernel arguments land; the epilogue is a template parameter, so the executed code is one
+//     short straight line;
+//   - wave w streams tiles kt = w, w + W, w + 2W, ... (4096^2: 3.89 -> 3.74 us);
+//   - all of a wave's tiles are loaded up front; a slot past the wave's tiles repeats its last
+//     tile on x zeroed instead of branching (a load under a branch is waited for at the join).
+// NRM (M = 1): x is the decoder layer's hidden state before its RMSNorm (OmniLlamaRMSNorm,
+// quant/omni_norm.py:52-63 of the reference) and the kernel applies the norm at the reference's
+// rounding point: each wave sums the squares of the x words it loads anyway (its own tiles;
+// together the waves cover the row once), the block combines the W sums through LDS behind a bare
+// s_barrier (no vmcnt drain), and every x word becomes RN16(weight * (x * rsqrt(mean + eps)))
+// (fp32 inside) before it is parked.  The x words and norm weights are issued before the codes
+// (in-order completion: the statistics wait for them, not for the weights).
 // ---------------------------------------------------------------------------------------------
 struct FastArgs {
   const uint32_t* qw;   // row tile 0 of qweight
@@ -592,20 +828,27 @@ struct FastArgs {
   int M, N, K, Kt, G;
   int W, lw;            // waves per block (power of two), log2 W
   uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
+  const float* nw;      // NRM: RMSNorm weight (fp32 [K]) applied to x first
+  float eps;
 };
 
-template <int BITS, int MT, int GPT, int ZM, int EP, int PF>
+template <int BITS, int MT, int GPT, int ZM, int EP, int PF, bool NRM = false>
 __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
+  __shared__ float nss[NRM ? kMaxWaves : 1];  // NRM: per-wave sums of squares
+  static_assert(!NRM || MT == 1, "the fused RMSNorm serves one token row");
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
   const int nt = blockIdx.x;
+  const _Float16* ax = a.x;
+  const _Float16* abias = a.bias;
+  _Float16* ay = a.y;
   const uint32_t* qw = a.qw + (int64_t)nt * a.Kt * (64 * BITS) + lane * BITS;
   const uint32_t* sz = a.qsz + (int64_t)nt * a.G * kTileN + n_in;
   constexpr int LPR = 64 / MT;  // lanes per x row
-  const _Float16* xr = a.x + (int64_t)min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
+  const _Float16* xr = ax + (int64_t)min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
   const int nts = (a.Kt - wave + a.W - 1) >> a.lw;  // >= 1: W <= Kt
   const int ktl = wave + ((nts - 1) << a.lw);        // the wave's last tile
   auto kt_of = [&](int i) { return min(wave + (i << a.lw), ktl); };
@@ -614,40 +857,92 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   };
   WTile<BITS, GPT> wt[PF];
   XRaw<MT> xq[PF];
-#pragma unroll
-  for (int u = 0; u < PF; ++u) wt[u].pc = load_piece_nt<BITS>(qw + kt_of(u) * (64 * BITS));
-#pragma unroll
-  for (int u = 0; u < PF; ++u) {
-    const int kt = kt_of(u);
+  float2 nwv[NRM ? PF : 1];  // NRM: norm weights of the lane's two x halves per tile
+  auto load_codes = [&](int u, int kt) { wt[u].pc = load_piece_nt<BITS>(qw + kt * (64 * BITS)); };
+  auto load_sz = [&](int u, int kt) {
     const int g0 = group_of_tile(kt);
 #pragma unroll
     for (int s = 0; s < GPT; ++s) wt[u].sz[s] = sz[(g0 + s) * kTileN];
+  };
+  auto load_x = [&](int u, int kt) {
     const _Float16* p = xr + kt * kTileK;
-    if constexpr (MT == 2) {
+    if constexpr (MT == 1) {
+      xq[u].w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (MT == 2) {
       const uint2 v = *reinterpret_cast<const uint2*>(p);
       xq[u].w[0] = v.x; xq[u].w[1] = v.y;
     } else {
       const uint4 v = *reinterpret_cast<const uint4*>(p);
       xq[u].w[0] = v.x; xq[u].w[1] = v.y; xq[u].w[2] = v.z; xq[u].w[3] = v.w;
     }
+  };
+  if constexpr (NRM) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      load_x(u, kt_of(u));
+      nwv[u] = *reinterpret_cast<const float2*>(a.nw + kt_of(u) * kTileK + 2 * lane);
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_sz(u, kt_of(u));
+  } else {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      load_sz(u, kt_of(u));
+      load_x(u, kt_of(u));
+    }
   }
-  // the epilogue's bias / residual operands, fetched while the weights stream (every wave loads,
-  // clamped: a load under a branch is waited for at the branch's join)
+  // the epilogue's bias / residual operands, fetched while the weights stream (fetched after the
+  // reduction they would cost one more round trip).  Only wave 0's lanes use them, but every wave
+  // loads (clamped, L2-resident): a load under a branch is waited for at the branch's join
   constexpr int NO = EP == kEpSiluMul ? MT * 8 : MT * kTileN;  // outputs per block
-  const int om = min(tid / (NO / MT), a.M - 1), on = tid % (NO / MT);
+  const int om = min(tid / (NO / MT), a.M - 1), on = tid % (NO / MT);  // output (row m, column n)
   const int64_t orow = (int64_t)nt * kTileN + on;
   const bool oval = tid < NO && tid / (NO / MT) < a.M && orow + (EP == kEpSiluMul ? 8 : 0) < a.N;
-  const _Float16* bsrc = a.bias ? a.bias + min(orow, (int64_t)a.N - 1) : a.x;
+  const _Float16* bsrc = abias ? abias + min(orow, (int64_t)a.N - 1) : ax;
   const _Float16 ob0 = bsrc[0];
-  const _Float16 ob1 = EP == kEpSiluMul ? bsrc[a.bias ? 8 : 0] : ob0;
+  const _Float16 ob1 = EP == kEpSiluMul ? bsrc[abias ? 8 : 0] : ob0;
   _Float16 ores = 0;
   if constexpr (EP == kEpResidual) ores = a.res[(int64_t)om * a.N + min(orow, (int64_t)a.N - 1)];
+
+  float rn = 1.f;  // NRM: rsqrt(mean(x^2) + eps)
+  if constexpr (NRM) {
+#pragma clang fp contract(off)
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (u < nts) {  // wave-uniform: slots past the wave's tiles repeat its last tile
+        const h2 v = as_h2(xq[u].w[0]);
+        const float f0 = (float)v.x, f1 = (float)v.y;
+        ss = ss + f0 * f0;
+        ss = ss + f1 * f1;
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) nss[wave] = ss;
+    // a bare s_barrier after the LDS store: __syncthreads() would also drain vmcnt, i.e. wait for
+    // the weight words still in flight; the waves only need each other's sums
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float tot = 0.f;
+    for (int w = 0; w < a.W; ++w) tot += nss[w];
+    rn = rsqrtf(tot / (float)a.K + a.eps);
+  }
 
   const Magics mg = make_magics<BITS>();
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   uint32_t* slot = &xs[wave][0];
   auto tile = [&](int u) {
     h8 xa[4];
+    if constexpr (NRM) {
+#pragma clang fp contract(off)
+      const h2 v = as_h2(xq[u].w[0]);
+      const float n0 = nwv[u].x * ((float)v.x * rn);
+      const float n1 = nwv[u].y * ((float)v.y * rn);
+      xq[u].w[0] = as_u32(h2{(_Float16)n0, (_Float16)n1});
+    }
     park_x<MT>(xa, xq[u], slot, lane, n_in);
     auto step = [&](auto S_) {
       constexpr int S = decltype(S_)::value;
@@ -690,17 +985,17 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
     const f4 p = r[0], q = r[1], c = r[2], d = r[3];
     const f4 e = (p + q) + (c + d);
     float t = (e[0] + e[1]) + (e[2] + e[3]);
-    if (a.bias) t += (float)b;
+    if (abias) t += (float)b;
     return (float)(_Float16)t;  // F.linear's fp16 output
   };
   if (oval) {  // wave 0 only (tid < NO <= 64)
     if constexpr (EP == kEpSiluMul) {  // 8 outputs per tile and row
       const float g = total(om * kTileN + on, ob0), u = total(om * kTileN + on + 8, ob1);
-      a.y[(int64_t)om * (a.N >> 1) + nt * 8 + on] = (_Float16)(silu_rn16(g) * u);
+      ay[(int64_t)om * (a.N >> 1) + nt * 8 + on] = (_Float16)(silu_rn16(g) * u);
     } else {
       float t = total(om * kTileN + on, ob0);
       if constexpr (EP == kEpResidual) t += (float)ores;
-      a.y[(int64_t)om * a.N + orow] = (_Float16)t;
+      ay[(int64_t)om * a.N + orow] = (_Float16)t;
     }
   }
 }
@@ -739,12 +1034,12 @@ __global__ __launch_bounds__(256) void dequant_kernel(
   one(std::integral_constant<int, 3>{});
 }
 
-inline uint32_t group_magic(int group) {
+static inline uint32_t group_magic(int group) {
   const uint64_t d = (uint64_t)(group / 32);
   return (uint32_t)(((1ull << 31) + d - 1) / d);
 }
 
-inline uint32_t tile_group_magic(int group) {  // GPT == 1: kt / (group / 128) = (kt * magic) >> 31
+static inline uint32_t tile_group_magic(int group) {  // GPT == 1: kt / (group / 128) = (kt * magic) >> 31
   const uint64_t c = group % kTileK == 0 ? (uint64_t)(group / kTileK) : 1;
   return (uint32_t)(((1ull << 31) + c - 1) / c);
 }
@@ -756,7 +1051,7 @@ inline uint32_t tile_group_magic(int group) {  // GPT == 1: kt / (group / 128) =
 #ifndef GEMV_WAVE_TARGET  // dev sweep knob (tools/dev/Makefile libgv*.so)
 #define GEMV_WAVE_TARGET 8192
 #endif
-inline int pick_waves(int Nt, int Kt, int& tpw) {
+static inline int pick_waves(int Nt, int Kt, int& tpw) {
   int W = 1;
   while (W < kMaxWaves && (int64_t)Nt * W < GEMV_WAVE_TARGET && (Nt < 512 || Kt >= 8 * W)) W *= 2;
   W = min(W, Kt);
@@ -795,8 +1090,74 @@ int launch_gemv(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   return (int)hipGetLastError();
 }
 
-inline bool group_fast(int K, int group) {  // whole-tile or 32 / 64-wide groups on whole k-tiles
+static inline bool group_fast(int K, int group) {  // whole-tile or 32 / 64-wide groups on whole k-tiles
   return K % kTileK == 0 && (group % kTileK == 0 || group == 32 || group == 64);
+}
+
+// ---- M == 1, wide matrices: the whole-row kernel ------------------------------------------------
+#ifndef GEMV_WROW_MIN_ROWS_CU  // dev knob: tile rows per CU from which the whole-row kernel runs
+#define GEMV_WROW_MIN_ROWS_CU 4
+#endif
+#ifndef GEMV_WROW_PF  // dev knob: tiles in flight per wave (gate/up: 8 15.3 us, 16 17.2 us;
+#define GEMV_WROW_PF 8  // tools/dev/rows_sweep.py, one box)
+#endif
+struct WrowGeo {
+  int rw, nb, pf;
+};
+// one tile row per wave where the rows fill the CUs (RW = ceil(rows / CU) waves per block, one
+// block per CU), more rows per wave beyond 8 per CU; PF tiles in flight, Kt % PF == 0
+static inline bool wrow_geometry(int64_t Nt, int Kt, int K, WrowGeo& g) {
+  const int64_t cus = device_cu_count();
+  if (Nt < GEMV_WROW_MIN_ROWS_CU * cus) return false;
+  g.pf = Kt % GEMV_WROW_PF == 0 ? GEMV_WROW_PF : (Kt % 8 == 0 ? 8 : 0);
+  if (!g.pf) return false;
+  g.rw = (int)std::min<int64_t>(kWrowMaxWaves, (Nt + cus - 1) / cus);
+  g.nb = (int)std::min<int64_t>(cus, (Nt + g.rw - 1) / g.rw);
+  // the x staging covers K / 8 chunks with kWrowXIter per thread
+  return (int64_t)g.rw * 64 * kWrowXIter * 8 >= K;
+}
+
+template <int BITS, int GPT, int ZM, bool NRM>
+int launch_wrow(const WrowArgs& a, const WrowGeo& g, hipStream_t st) {
+  const size_t lds = (size_t)a.K * 2;
+#define QLIN_WR(P)                                                                             \
+  hipLaunchKernelGGL((gemv_wrow_kernel<BITS, GPT, ZM, P, NRM>), dim3((unsigned)g.nb),           \
+                     dim3(64 * g.rw), lds, st, a)
+  if (g.pf == 16) QLIN_WR(16);
+  else QLIN_WR(8);
+#undef QLIN_WR
+  return (int)hipGetLastError();
+}
+
+template <int BITS, int ZM>
+int launch_wrow_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
+                  uint16_t* y, int N, int K, int group, hipStream_t st, int ep,
+                  const uint16_t* res, const float* nw, float eps, const WrowGeo& g) {
+  WrowArgs a;
+  a.qw = qw;
+  a.qsz = qsz;
+  a.x = (const _Float16*)x;
+  a.has_bias = bias != nullptr;
+  a.bias = (const _Float16*)(bias ? bias : y);
+  a.res = (const _Float16*)(ep == kEpResidual ? res : y);
+  a.nres = ep == kEpSiluMul ? N / 2 : N;
+  a.y = (_Float16*)y;
+  a.nw = nw;
+  a.eps = eps;
+  a.ep = ep;
+  a.N = N;
+  a.K = K;
+  a.Kt = K / kTileK;
+  a.G = K / group;
+  a.Nt = (N + kTileN - 1) / kTileN;
+  a.nwaves = g.nb * g.rw;
+  a.cmagic = tile_group_magic(group);
+#define QLIN_WG(GPT)                                                                            \
+  return nw ? launch_wrow<BITS, GPT, ZM, true>(a, g, st) : launch_wrow<BITS, GPT, ZM, false>(a, g, st)
+  if (group % kTileK == 0) QLIN_WG(1);
+  if (group == 64) QLIN_WG(2);
+  QLIN_WG(4);
+#undef QLIN_WG
 }
 
 // ---- M == 1: the rows kernel ------------------------------------------------------------------
@@ -805,47 +1166,51 @@ struct RowsGeo {
 };
 
 // W * TPW == Kt with TPW the smallest of {2, 4, 8} that keeps W <= 16 (the most waves per row);
-// one row per block up to 2 rows per CU, else a persistent grid of GEMV_ROWS_BPC blocks per CU;
-// PF = the wave's whole row (one-row blocks) or 4 / 8 tiles across rows
+// one row per block up to 2 rows per CU (PF = the wave's whole row), else a persistent grid of
+// GEMV_ROWS_BPC blocks per CU streaming 8 tiles ahead across rows
 #ifndef GEMV_ROWS_MINTPW  // dev knob: smallest k-tiles per wave and row
 #define GEMV_ROWS_MINTPW 2
 #endif
-inline bool rows_geometry(int64_t Nt, int Kt, RowsGeo& g) {
+#ifndef GEMV_ROWS_ONEROW_CU  // dev knob: grids of up to this many rows per CU run one row per block
+#define GEMV_ROWS_ONEROW_CU 2
+#endif
+static inline bool rows_geometry(int64_t Nt, int Kt, RowsGeo& g) {
+  const int64_t cus = device_cu_count();
+  // one-row grids: few enough waves that every block is resident at once (16 waves per CU: the
+  // register budget of these kernels admits at least that); measured qkv (384 rows) W = 16: two
+  // rounds of blocks, 7.4 us; W = 8: 6.1 us (tools/dev/rows_stamps.py, rows_sweep.py)
+  const bool onerow = Nt <= GEMV_ROWS_ONEROW_CU * cus;
   g.TPW = 0;
   for (int t = GEMV_ROWS_MINTPW; t <= kRowsMaxTPW; t *= 2)
-    if (Kt % t == 0 && Kt / t <= kMaxWaves) {
+    if (Kt % t == 0 && Kt / t <= kMaxWaves && (!onerow || t == kRowsMaxTPW ||
+                                               Nt * (Kt / t) <= kMaxWaves * cus)) {
       g.TPW = t;
       break;
     }
   if (!g.TPW || Nt < 1 || Nt > (1 << 26)) return false;
   g.W = Kt / g.TPW;
-  const int64_t cus = device_cu_count();
-  g.nb = Nt <= 2 * cus ? (int)Nt : (int)(cus * GEMV_ROWS_BPC);
-  const int64_t tmin = (Nt / g.nb) * g.TPW;  // fewest tiles any wave streams
-  g.pf = 2;
-  while (g.pf * 2 <= GEMV_ROWS_MAXPF && g.pf * 2 <= tmin) g.pf *= 2;
+  g.nb = onerow ? (int)Nt : (int)(cus * GEMV_ROWS_BPC);
+  g.pf = (g.nb < Nt && GEMV_ROWS_MAXPF >= 8 && (Nt / g.nb) * g.TPW >= 8) ? 8 : g.TPW;
   return true;
 }
 
-inline bool rows_ok(int M, int K, int group, const Ep& e) {
-  RowsGeo g;
-  return M == 1 && !e.aq.on && group_fast(K, group) && rows_geometry(1, K / kTileK, g);
-}
 
-template <int BITS, int GPT, int ZM>
-int launch_rows(RowsArgs a, const RowsGeo& g, hipStream_t st) {
-  a.W = g.W;
-  a.TPW = g.TPW;
-  a.nb = g.nb;
-  a.kt0m = GEMV_ROWS_CONTIG ? g.TPW : 1;
-  a.kts = GEMV_ROWS_CONTIG ? 1 : g.W;
-  const size_t lds = (size_t)g.W * g.TPW * 64 * sizeof(uint32_t);
-#define QLIN_GR(PF)                                                                             \
-  hipLaunchKernelGGL((gemv_rows_kernel<BITS, GPT, ZM, PF>), dim3((unsigned)g.nb), dim3(64 * g.W), \
-                     lds, st, a)
-  if (g.pf >= 8) QLIN_GR(8);
-  else if (g.pf == 4) QLIN_GR(4);
-  else QLIN_GR(2);
+template <int BITS, int GPT, int ZM, bool NRM>
+int launch_rows(const RowsArgs& a, const RowsGeo& g, hipStream_t st) {
+  size_t lds = 0;
+  if (g.nb < a.N / kTileN && GEMV_ROWS_LDS_MIN > 0) lds = GEMV_ROWS_LDS_MIN;
+#define QLIN_GR(T, P)                                                                          \
+  hipLaunchKernelGGL((gemv_rows_kernel<BITS, GPT, ZM, T, P, NRM>), dim3((unsigned)g.nb),        \
+                     dim3(64 * g.W), lds, st, a)
+  if (g.TPW == 2) {
+    if (g.pf == 8) QLIN_GR(2, 8);
+    else QLIN_GR(2, 2);
+  } else if (g.TPW == 4) {
+    if (g.pf == 8) QLIN_GR(4, 8);
+    else QLIN_GR(4, 4);
+  } else {
+    QLIN_GR(8, 8);
+  }
 #undef QLIN_GR
   return (int)hipGetLastError();
 }
@@ -853,70 +1218,95 @@ int launch_rows(RowsArgs a, const RowsGeo& g, hipStream_t st) {
 template <int BITS, int ZM>
 int launch_rows_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int N, int K, int group, hipStream_t st, int ep,
-                  const uint16_t* res, const float* nw, float eps) {
-  RowsGeo g;
+                  const uint16_t* res, const float* nw, float eps, const RowsGeo& g) {
   const int64_t Nt = (N + kTileN - 1) / kTileN;
-  if (!rows_geometry(Nt, K / kTileK, g)) return QLIN_EINVAL;
   RowsArgs a;
   a.qw = qw;
   a.qsz = qsz;
   a.x = (const _Float16*)x;
-  a.bias = (const _Float16*)bias;
-  a.res = (const _Float16*)res;
+  // absent epilogue operands point at y (read before it is written, never used)
+  const int ny = ep == kEpSiluMul ? N / 2 : N;
+  a.has_bias = bias != nullptr;
+  a.bias = (const _Float16*)(bias ? bias : y);
+  a.res = (const _Float16*)(ep == kEpResidual ? res : y);
+  a.nres = ny;
   a.y = (_Float16*)y;
   a.nw = nw;
   a.eps = eps;
   a.ep = ep;
-  a.nrm = nw != nullptr;
   a.N = N;
   a.K = K;
   a.Kt = K / kTileK;
   a.G = K / group;
-  a.Nt = (int)Nt;
+  a.W = g.W;
+  a.nb = g.nb;
+  a.rpb = (int)(Nt / g.nb);
+  a.extra = (int)(Nt % g.nb);
+  a.wstep = (int64_t)g.nb * a.Kt * 64 * BITS;
+  a.sstep = (int64_t)g.nb * a.G * kTileN;
   a.cmagic = tile_group_magic(group);
-  if (group % kTileK == 0) return launch_rows<BITS, 1, ZM>(a, g, st);
-  if (group == 64) return launch_rows<BITS, 2, ZM>(a, g, st);
-  return launch_rows<BITS, 4, ZM>(a, g, st);
+#ifdef GEMV_ROWS_STAMP
+  a.stamps = g_rows_stamps;
+#endif
+#define QLIN_RG(GPT)                                                                            \
+  return nw ? launch_rows<BITS, GPT, ZM, true>(a, g, st) : launch_rows<BITS, GPT, ZM, false>(a, g, st)
+  if (group % kTileK == 0) QLIN_RG(1);
+  if (group == 64) QLIN_RG(2);
+  QLIN_RG(4);
+#undef QLIN_RG
 }
 
-// ---- M == 2..4: the fast kernel --------------------------------------------------------------
-inline bool fast_ok(int M, int K, int group, const Ep& e) {
-  return M >= 2 && M <= 4 && !e.aq.on && group_fast(K, group);
-}
-
+// ---- M <= 4: the fast kernel -----------------------------------------------------------------
 template <int BITS, int MT, int GPT, int ZM, int EP>
 int launch_fast_t(const FastArgs& a, int Nt, int tpw, hipStream_t st) {
-#define QLIN_GF(PF)                                                                          \
-  hipLaunchKernelGGL((gemv_fast_kernel<BITS, MT, GPT, ZM, EP, PF>), dim3(Nt), dim3(64 * a.W), \
-                     0, st, a)
-  if (tpw <= 2) QLIN_GF(2);
-  else QLIN_GF(4);
+#define QLIN_GF(PF, NR)                                                                      \
+  hipLaunchKernelGGL((gemv_fast_kernel<BITS, MT, GPT, ZM, EP, PF, NR>), dim3(Nt),          \
+                     dim3(64 * a.W), 0, st, a)
+  if constexpr (MT == 1) {
+    if (a.nw) {
+      if (tpw <= 2) QLIN_GF(2, true);
+      else QLIN_GF(4, true);
+      return (int)hipGetLastError();
+    }
+  }
+  if (tpw <= 2) QLIN_GF(2, false);
+  else QLIN_GF(4, false);
 #undef QLIN_GF
   return (int)hipGetLastError();
 }
 
-// fast-path geometry: pick_waves rounded down to a power of two; the fast path takes launches
-// whose waves stream at most 4 tiles (tools/dev/fast_geo.py)
-inline bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
+// fast-path geometry: pick_waves rounded down to a power of two, then halved while the grid holds
+// more than 16 waves per CU (all blocks resident in one round: q/k/v, 384 row tiles, W = 16 ran in
+// two rounds, tools/dev/rows_stamps.py); the fast path takes launches whose waves stream at most 4
+// tiles (tools/dev/fast_geo.py)
+static inline bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
   W = pick_waves(Nt, Kt, tpw);
   lw = 0;
   while ((2 << lw) <= W) ++lw;  // round W down to a power of two (W <= Kt)
+  const int64_t cus = device_cu_count();
+  while (lw > 0 && (int64_t)Nt * (1 << lw) > kMaxWaves * cus && (Kt + (1 << lw) / 2 - 1) / ((1 << lw) / 2) <= 4)
+    --lw;
   W = 1 << lw;
   tpw = (Kt + W - 1) / W;
   return tpw <= 4;
 }
 
+static inline bool fast_ok(int M, int K, int group, const Ep& e) {
+  return M <= 4 && !e.aq.on && group_fast(K, group);
+}
+
 template <int BITS, int MT, int ZM>
 int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                 uint16_t* y, int M, int N, int K, int group, int W, int lw, int tpw,
-                hipStream_t st, const Ep& e) {
+                hipStream_t st, int ep, const uint16_t* res, const float* nw = nullptr,
+                float eps = 0.f) {
   const int Nt = (N + kTileN - 1) / kTileN;
   FastArgs a;
   a.qw = qw;
   a.qsz = qsz;
   a.x = (const _Float16*)x;
   a.bias = (const _Float16*)bias;
-  a.res = (const _Float16*)e.res;
+  a.res = (const _Float16*)res;
   a.y = (_Float16*)y;
   a.M = M;
   a.N = N;
@@ -926,14 +1316,54 @@ int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   a.W = W;
   a.lw = lw;
   a.cmagic = tile_group_magic(group);
+  a.nw = nw;
+  a.eps = eps;
 #define QLIN_FE(GPT)                                                                           \
-  return e.ep == kEpResidual  ? launch_fast_t<BITS, MT, GPT, ZM, kEpResidual>(a, Nt, tpw, st)  \
-         : e.ep == kEpSiluMul ? launch_fast_t<BITS, MT, GPT, ZM, kEpSiluMul>(a, Nt, tpw, st)   \
-                              : launch_fast_t<BITS, MT, GPT, ZM, kEpNone>(a, Nt, tpw, st)
+  return ep == kEpResidual  ? launch_fast_t<BITS, MT, GPT, ZM, kEpResidual>(a, Nt, tpw, st)  \
+         : ep == kEpSiluMul ? launch_fast_t<BITS, MT, GPT, ZM, kEpSiluMul>(a, Nt, tpw, st)   \
+                            : launch_fast_t<BITS, MT, GPT, ZM, kEpNone>(a, Nt, tpw, st)
   if (group % kTileK == 0) QLIN_FE(1);
   if (group == 64) QLIN_FE(2);
   QLIN_FE(4);
 #undef QLIN_FE
+}
+
+// ---- M == 1 routing: each decode shape on the kernel measured fastest for it
+// (tools/dev/rows_sweep.py: gate/up 28,672 x 4,096 whole-row 15.3 us vs fast 15.4 / rows 15.6;
+// down 4,096 x 14,336 rows 8.25 us vs gemv_kernel 8.7; 4096^2 and q/k/v fast 3.7 / 5.7 us vs rows
+// 3.8-4.2 / 6.1)
+enum { kM1None = 0, kM1Wrow, kM1Fast, kM1Rows };
+static inline int m1_route(int64_t N, int K, int group, const void* x, const float* nw, WrowGeo& wg,
+                           int& W, int& lw, int& tpw, RowsGeo& rg) {
+  if (!group_fast(K, group)) return kM1None;
+  const int64_t Nt = (N + kTileN - 1) / kTileN;
+  const int Kt = K / kTileK;
+  if (((uintptr_t)x & 15) == 0 && ((uintptr_t)nw & 15) == 0 && K % 8 == 0 &&
+      wrow_geometry(Nt, Kt, K, wg))
+    return kM1Wrow;
+  if (Nt <= (1 << 26) && fast_geometry((int)Nt, Kt, W, lw, tpw)) return kM1Fast;
+  if (rows_geometry(Nt, Kt, rg)) return kM1Rows;
+  return kM1None;
+}
+
+template <int BITS, int ZM>
+int launch_m1(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
+              uint16_t* y, int N, int K, int group, hipStream_t st, int ep, const uint16_t* res,
+              const float* nw, float eps) {
+  WrowGeo wg;
+  RowsGeo rg;
+  int W = 0, lw = 0, tpw = 0;
+  switch (m1_route(N, K, group, x, nw, wg, W, lw, tpw, rg)) {
+    case kM1Wrow:
+      return launch_wrow_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, ep, res, nw, eps, wg);
+    case kM1Fast:
+      return launch_fast<BITS, 1, ZM>(qw, qsz, x, bias, y, 1, N, K, group, W, lw, tpw, st, ep,
+                                      res, nw, eps);
+    case kM1Rows:
+      return launch_rows_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, ep, res, nw, eps, rg);
+    default:
+      return QLIN_EINVAL;
+  }
 }
 
 template <int BITS, int MT, int ZM>
@@ -949,14 +1379,19 @@ int launch_gemv_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
 template <int BITS, int ZM>
 int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int M, int N, int K, int group, hipStream_t st, const Ep& e) {
-  if (rows_ok(M, K, group, e))
-    return launch_rows_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, e.ep, e.res, nullptr,
-                                   0.f);
+  if (M == 1 && !e.aq.on) {
+    WrowGeo wg;
+    RowsGeo rg;
+    int W = 0, lw = 0, tpw = 0;
+    if (m1_route(N, K, group, x, nullptr, wg, W, lw, tpw, rg) != kM1None)
+      return launch_m1<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, e.ep, e.res, nullptr, 0.f);
+  }
   int W = 0, lw = 0, tpw = 0;
-  if (fast_ok(M, K, group, e) &&
+  if (M > 1 && fast_ok(M, K, group, e) &&
       fast_geometry((N + kTileN - 1) / kTileN, K / kTileK, W, lw, tpw)) {
-    if (M == 2) return launch_fast<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, W, lw, tpw, st, e);
-    return launch_fast<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, W, lw, tpw, st, e);
+    if (M == 2)
+      return launch_fast<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, W, lw, tpw, st, e.ep, e.res);
+    return launch_fast<BITS, 4, ZM>(qw, qsz, x, bias, y, M, N, K, group, W, lw, tpw, st, e.ep, e.res);
   }
   if (M == 1) return launch_gemv_g<BITS, 1, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
   if (M == 2) return launch_gemv_g<BITS, 2, ZM>(qw, qsz, x, bias, y, M, N, K, group, st, e);
@@ -974,10 +1409,10 @@ int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   EXT template int qlin_gv::launch_gemv_m<B, Z>(const uint32_t*, const uint32_t*, const uint16_t*, \
                                                 const uint16_t*, uint16_t*, int, int, int, int,    \
                                                 hipStream_t, const qlin_gv::Ep&);                \
-  EXT template int qlin_gv::launch_rows_g<B, Z>(const uint32_t*, const uint32_t*, const uint16_t*, \
-                                                const uint16_t*, uint16_t*, int, int, int,         \
-                                                hipStream_t, int, const uint16_t*, const float*,   \
-                                                float)
+  EXT template int qlin_gv::launch_m1<B, Z>(const uint32_t*, const uint32_t*, const uint16_t*,  \
+                                            const uint16_t*, uint16_t*, int, int, int,           \
+                                            hipStream_t, int, const uint16_t*, const float*,     \
+                                            float)
 #define QLIN_GV_INST_B(EXT, B)           \
   QLIN_GV_INST(EXT, B, kZNarrow);        \
   QLIN_GV_INST(EXT, B, kZWide);          \
@@ -1056,8 +1491,10 @@ namespace qlin_gv {
 // 32 / 64-wide groups, Kt = W * TPW with W <= 16, TPW in {2, 4, 8})
 bool rmsnorm_linear_ok(int64_t M, int64_t N, int64_t K, int bits, int group) {
   if (M != 1 || N < 1 || !valid_layout(N, K, bits, group)) return false;
-  const Ep e{nullptr, kEpNone, ActQ{false, 0, 0, 0.f, 0.f}};
-  return rows_ok(1, (int)K, group, e);
+  WrowGeo wg;
+  RowsGeo rg;
+  int W = 0, lw = 0, tpw = 0;
+  return m1_route(N, (int)K, group, nullptr, nullptr, wg, W, lw, tpw, rg) != kM1None;
 }
 }  // namespace
 
@@ -1080,12 +1517,12 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
   const int n = (int)N, k = (int)K;
   const int zm = zero_mode(flags);
 #define QLIN_N(B)                                                                              \
-  return zm == kZFloat ? launch_rows_g<B, kZFloat>(qweight, qsz, x, bias, y, n, k, group, st,  \
-                                                   epilogue, residual, norm_weight, eps)       \
-         : zm == kZWide ? launch_rows_g<B, kZWide>(qweight, qsz, x, bias, y, n, k, group, st,  \
-                                                   epilogue, residual, norm_weight, eps)       \
-                        : launch_rows_g<B, kZNarrow>(qweight, qsz, x, bias, y, n, k, group, st, \
-                                                     epilogue, residual, norm_weight, eps)
+  return zm == kZFloat ? launch_m1<B, kZFloat>(qweight, qsz, x, bias, y, n, k, group, st,  \
+                                               epilogue, residual, norm_weight, eps)       \
+         : zm == kZWide ? launch_m1<B, kZWide>(qweight, qsz, x, bias, y, n, k, group, st,  \
+                                               epilogue, residual, norm_weight, eps)       \
+                        : launch_m1<B, kZNarrow>(qweight, qsz, x, bias, y, n, k, group, st, \
+                                                 epilogue, residual, norm_weight, eps)
   switch (bits) {
     case 2: QLIN_N(2);
     case 3: QLIN_N(3);
@@ -1094,6 +1531,10 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
   }
 #undef QLIN_N
 }
+
+#ifdef GEMV_ROWS_STAMP
+extern "C" void qlin_dev_rows_stamps(uint64_t* p) { qlin_gv::g_rows_stamps = p; }
+#endif
 
 extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                              const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,

@@ -20,9 +20,16 @@ of |diff| / max |logit| (``p99``) and top-1 agreement.  A float64 evaluation of 
 mathematics (no intermediate roundings) anchors accuracy.
 
 On random-init stacks an fp16 ulp flip anywhere is amplified layer after layer: the reference
-differs from its own reordered twin by more than 1e-3 of max |logit| (the order floor).  The bar
- on every seed: each packed / fused path's max and p99 distance to the
-fake-quant logits <= 1.1 x the floor's, and its error against float64 <= 1.1 x the reference's.
+differs from its own reordered twins by more than 1e-3 of max |logit|.  The twins run the SAME
+reference arithmetic (fp16 products of the same W_dq and activations, one fp16 rounding of every
+linear output) with only the summation order of F.linear changed:
+  fake_quant_f32lin   F.linear on fp32 copies (hipBLASLt's fp32 kernel order);
+  fake_quant_ksplit   the same in two K halves added in fp32 (another association);
+  fake_quant_f64acc   the sum accumulated in float64 (the exactly rounded order).
+The order floor is the largest distance of a twin to the fake-quant logits (each twin's own
+distance is reported beside it).  The bar on every seed: each packed / fused
+path's max and p99 distance to the fake-quant logits <= 1.1 x the floor's, and its error against
+float64 <= 1.1 x the reference's.
 Numbers are written to $QLIN_PARITY_OUT (profiles/r4_decode_parity.json, r4_prefill_parity.json,
 r4_prefill32_parity.json)."""
 import json
@@ -142,10 +149,26 @@ def _f32_linear(x, w, b=None):
     return F.linear(x.float(), w.float(), None if b is None else b.float()).to(x.dtype)
 
 
-def _reorder_reference(model, on):
+def _ksplit_linear(x, w, b=None):
+    """The same with K summed as two halves added in fp32 (another association)."""
+    h = x.shape[-1] // 2
+    y = F.linear(x[..., :h].float(), w[:, :h].float()) + F.linear(x[..., h:].float(), w[:, h:].float())
+    return (y if b is None else y + b.float()).to(x.dtype)
+
+
+def _f64acc_linear(x, w, b=None):
+    """The same accumulated in float64 (the exactly rounded sum of the fp16 products)."""
+    return F.linear(x.double(), w.double(), None if b is None else b.double()).to(x.dtype)
+
+
+TWINS = {"fake_quant_f32lin": _f32_linear, "fake_quant_ksplit": _ksplit_linear,
+         "fake_quant_f64acc": _f64acc_linear}
+
+
+def _reorder_reference(model, fn):
     for m in model.modules():
         if isinstance(m, QuantLinear) and not m.packed:
-            m.fwd_func = _f32_linear if on else F.linear
+            m.fwd_func = fn
 
 
 def _progress(*a):
@@ -168,21 +191,21 @@ def _report(seed, paths, model, cfg, ref64_h):
     return rep
 
 
-def _judge(reps, ref_name="fake_quant", floor_name="fake_quant_f32lin", out_env=None):
-    """Per seed: every other path within BAR x the order floor (max and p99) and BAR x the
-    reference's own float64 error."""
+def _judge(reps, ref_name="fake_quant", out_env=None):
+    """Per seed: every other path within BAR x the order floor (the twins' largest distance to
+    the fake-quant logits, max and p99 separately) and BAR x the reference's own float64 error."""
     failures = []
     for rep in reps:
-        fl = rep[floor_name]
         fq = rep[ref_name]
-        crit = {"max_vs_fake_quant": BAR * fl["logits_max_vs_fake_quant"],
-                "p99_vs_fake_quant": BAR * fl["logits_p99_vs_fake_quant"],
+        fmax = max(rep[t]["logits_max_vs_fake_quant"] for t in TWINS)
+        fp99 = max(rep[t]["logits_p99_vs_fake_quant"] for t in TWINS)
+        crit = {"max_vs_fake_quant": BAR * fmax, "p99_vs_fake_quant": BAR * fp99,
                 "err_vs_fp64": BAR * fq["logits_err_vs_fp64"],
-                "order_floor_max": fl["logits_max_vs_fake_quant"],
-                "order_floor_p99": fl["logits_p99_vs_fake_quant"]}
+                "order_floor_max": fmax, "order_floor_p99": fp99,
+                "order_floor_twins_max": {t: rep[t]["logits_max_vs_fake_quant"] for t in TWINS}}
         rep["criteria"] = crit
         for name, r in rep.items():
-            if name in (ref_name, floor_name, "criteria", "seed") or not isinstance(r, dict):
+            if name in (ref_name, "criteria", "seed") or name in TWINS or not isinstance(r, dict):
                 continue
             r["ratio_max_to_floor"] = r["logits_max_vs_fake_quant"] / crit["order_floor_max"]
             r["ratio_p99_to_floor"] = r["logits_p99_vs_fake_quant"] / crit["order_floor_p99"]
@@ -234,9 +257,10 @@ def _decode_seed(seed):
         return h[0, 0]
 
     paths = {"fake_quant": run()}
-    _reorder_reference(model, True)
-    paths["fake_quant_f32lin"] = run()
-    _reorder_reference(model, False)
+    for name, fn in TWINS.items():
+        _reorder_reference(model, fn)
+        paths[name] = run()
+    _reorder_reference(model, F.linear)
     for layer in model.layers:
         pack_quant_linears(layer)
     paths["packed"] = run()
@@ -280,9 +304,10 @@ def _prefill_seed(seed, layers, S):
         return h[0]
 
     paths = {"fake_quant": run()}
-    _reorder_reference(model, True)
-    paths["fake_quant_f32lin"] = run()
-    _reorder_reference(model, False)
+    for name, fn in TWINS.items():
+        _reorder_reference(model, fn)
+        paths[name] = run()
+    _reorder_reference(model, F.linear)
     for layer in model.layers:
         pack_quant_linears(layer)
     paths["packed"] = run()

@@ -180,3 +180,24 @@ def test_product_path_never_imports_the_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in src.replace("oracle/", ""), f
+
+
+def test_integration_stub_matches_the_header_abi():
+    """The reference-side binding in INTEGRATION.md asserts the ABI version the header declares."""
+    hdr = open(HEADER).read()
+    abi = int(re.search(r"#define QLIN_ABI_VERSION (\d+)", hdr).group(1))
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    stubs = re.findall(r"qlin_abi_version\(\) == (\d+)", doc)
+    assert stubs and all(int(v) == abi for v in stubs), (stubs, abi)
+
+
+def test_mask_cache_does_not_keep_masks_alive():
+    import gc
+    import weakref
+    from quant import qlin
+    m = torch.triu(torch.full((4, 4), -6e4), 1).half()[None, None]
+    qlin.mask_is_causal(m, 4, 4)
+    r = weakref.ref(m)
+    del m
+    gc.collect()
+    assert r() is None
