@@ -28,6 +28,9 @@
 // and sums run in a different order than hipBLASLt's bmm and the softmax is merged across chunks
 // (exp(m_c - M) rescaling), so results agree with the reference to fp32 rounding, not bit for bit.
 #include "qlin_common.h"  // QLIN_OK / QLIN_EINVAL
+#include "qlin_gemv_tile.h"  // packed-tile helpers of the fused o_proj (attn_o_kernel)
+
+#include <algorithm>
 #include "../../include/qlin_gfx950.h"
 
 namespace {
@@ -110,13 +113,38 @@ struct RopeIn {
   _Float16* vc;
 };
 
+struct AttnArgs {
+  const float* q;
+  const _Float16* k;
+  const _Float16* v;
+  const _Float16* mask;
+  void* out;
+  int out_f16, Hq, Hkv, L;
+  int64_t kv_hs;
+  int chunk, S;
+  float scale_div;
+  int* counters;
+  float* part_o;
+  float* part_ml;
+  RopeIn ri;
+  int* done;  // attn_o: kDoneReplicas completion counters, each += 1 per merged (b, kv head)
+};
+constexpr int kDoneReplicas = 8;  // one 128-B line each (32 ints apart)
+
 template <int GRP, bool ROPE = false>
-__global__ __launch_bounds__(kThreads) void attn_decode_kernel(
-    const float* __restrict__ q, const _Float16* __restrict__ k, const _Float16* __restrict__ v,
-    const _Float16* __restrict__ mask, void* __restrict__ out, int out_f16, int Hq, int Hkv,
-    int L, int64_t kv_hs, int chunk,
-    int S, float scale_div, int* __restrict__ counters, float* __restrict__ part_o,
-    float* __restrict__ part_ml, const RopeIn ri) {
+__device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh, const int split) {
+  const float* __restrict__ q = A.q;
+  const _Float16* __restrict__ k = A.k;
+  const _Float16* __restrict__ v = A.v;
+  const _Float16* __restrict__ mask = A.mask;
+  void* __restrict__ out = A.out;
+  const int out_f16 = A.out_f16, Hq = A.Hq, Hkv = A.Hkv, L = A.L, chunk = A.chunk, S = A.S;
+  const int64_t kv_hs = A.kv_hs;
+  const float scale_div = A.scale_div;
+  int* __restrict__ counters = A.counters;
+  float* __restrict__ part_o = A.part_o;
+  float* __restrict__ part_ml = A.part_ml;
+  const RopeIn& ri = A.ri;
   __shared__ float qs[GRP][kD];
   __shared__ __attribute__((aligned(16))) _Float16 knew[ROPE ? kD : 8];  // ROPE: the new k row
   __shared__ __attribute__((aligned(16))) _Float16 vnew[ROPE ? kD : 8];  // ... and v row
@@ -127,9 +155,7 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
   __shared__ float ml_l[kMaxSplit][GRP];   // merge: chunk sums
   __shared__ int last;
 
-  const int bh = blockIdx.x;  // b * Hkv + kv head
-  const int split = blockIdx.y;
-  const int b = bh / Hkv, hk = bh % Hkv;
+  const int b = bh / Hkv, hk = bh % Hkv;  // bh = b * Hkv + kv head
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int sub = tid & 7, tl = tid >> 3;  // score passes: 8 lanes x 16 dims per K row
   const int t0 = split * chunk;
@@ -316,9 +342,29 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
     if (out_f16) reinterpret_cast<_Float16*>(out)[qh0 * kD + o] = (_Float16)val;
     else reinterpret_cast<float*>(out)[qh0 * kD + o] = val;
   };
-  if (S == 1) {
+  // attn_o (done != null, fp16 out): the output row stored write-through (sc1) as fp16 pairs,
+  // drained, then counted into every completion replica by one lane (the o_proj blocks of the
+  // same launch poll them, then read the row with sc1 loads; MI355X_MICROARCH.md hand-off table)
+  auto put_all = [&]() {
+    if (A.done) {
+      uint32_t* o32 = reinterpret_cast<uint32_t*>(reinterpret_cast<_Float16*>(out) + qh0 * kD);
+      for (int o = 2 * tid; o < GRP * kD; o += 2 * kThreads) {
+        const float v0 = (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD];
+        const float v1 = (po[0][o + 1] + po[1][o + 1] + po[2][o + 1] + po[3][o + 1]) / cl[o / kD];
+        __hip_atomic_store(o32 + o / 2, qlin::as_u32(qlin::h2{(_Float16)v0, (_Float16)v1}),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid < kDoneReplicas)
+        __hip_atomic_fetch_add(A.done + 32 * tid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     for (int o = tid; o < GRP * kD; o += kThreads)
       put(o, (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD]);
+  };
+  if (S == 1) {
+    put_all();
     return;
   }
 
@@ -416,9 +462,13 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(
     for (int j = 0; j < J; ++j) po[wave][lane + 64 * j] = acc[j];
   }
   __syncthreads();
-  for (int o = tid; o < GRP * kD; o += kThreads)
-    put(o, (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD]);
   if (tid == 0) counters[bh] = 0;  // ready for the next launch (graph replay)
+  put_all();
+}
+
+template <int GRP, bool ROPE = false>
+__global__ __launch_bounds__(kThreads) void attn_decode_kernel(const AttnArgs A) {
+  attn_decode_body<GRP, ROPE>(A, blockIdx.x, blockIdx.y);
 }
 
 int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
@@ -427,11 +477,11 @@ int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const ui
                   const Split& sp, hipStream_t st, const RopeIn& ri) {
   const dim3 grid((unsigned)(B * Hkv), (unsigned)sp.S);
   const int grp = Hq / Hkv;
-#define QLIN_A(G, R)                                                                          \
-  hipLaunchKernelGGL((attn_decode_kernel<G, R>), grid, dim3(kThreads), 0, st, q,              \
-                     (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,        \
-                     out_dtype == QLIN_F16, Hq, Hkv, (int)L, kv_hs, sp.chunk, sp.S, scale_div,  \
-                     (int*)counters, part_o, part_ml, ri)
+  const AttnArgs A{q, (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,
+                   out_dtype == QLIN_F16, Hq, Hkv, (int)L, kv_hs, sp.chunk, sp.S, scale_div,
+                   (int*)counters, part_o, part_ml, ri, nullptr};
+#define QLIN_A(G, R) \
+  hipLaunchKernelGGL((attn_decode_kernel<G, R>), grid, dim3(kThreads), 0, st, A)
 #define QLIN_AR(G)                \
   if (ri.q16) QLIN_A(G, true);    \
   else QLIN_A(G, false);          \
@@ -542,4 +592,248 @@ extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, co
 extern "C" int qlin_attn_decode_splits(int64_t B, int Hkv, int64_t L) {
   if (B < 1 || Hkv < 1 || L < 1 || L > kMaxL) return -1;
   return choose_split(B, Hkv, L).S;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode attention + o_proj (+ residual) in ONE launch (qlin_attn_decode_o_f16, batch 1).
+//
+// The reference's o_proj(attn_output) and the decoder layer's residual add
+// (models/int_llama_layer.py:174, :249) read the attention output, a grid-wide dependency: as two
+// launches the o_proj GEMV pays a kernel boundary and then its weights' HBM round trip only after
+// the attention has finished.  Here the grid holds the attention blocks (split-L, as
+// qlin_attn_decode_rope; dispatched first: lower block indices) and one o_proj block per 16-row
+// tile of o_proj; an o_proj block issues all its packed weight tiles at once (the whole 8.8 MB of
+// a 4096 x 4096 int4 o_proj is in flight while the attention computes), then waits for the
+// attention: every merged (b, kv head) output row is stored write-through (sc1) and counted into
+// kDoneReplicas completion counters; one lane of each o_proj block polls its replica with sc1
+// loads (s_sleep between polls), then the block reads the attention row with sc1 loads and
+// finishes the GEMV: exact W_dq, one MFMA chain per wave, the 4 wave partials added in a fixed
+// order, F.linear's fp16 output, + residual (one fp16 rounding).  The last o_proj block to pass
+// its wait resets the counters (graph-replayable, no memset).  A wait is bounded: after
+// ~0.1 s it sets the workspace error word and proceeds (wrong output, no hang).
+// Deadlock freedom: the attention blocks never wait for o_proj blocks and are dispatched first.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kOTpw = 8;           // o_proj k-tiles per wave (4 waves: K <= 32 x 128)
+constexpr int kWsDone = 0;         // workspace offsets (bytes)
+constexpr int kWsConsumed = 1024;
+constexpr int kWsErr = 1152;
+constexpr int kWsCounters = 1280;  // attention merge counters, int32 [Hkv]
+
+struct OArgs {
+  const uint32_t* qw;
+  const uint32_t* qsz;
+  const _Float16* bias;  // never null (points at residual when absent; has_bias says)
+  const _Float16* res;
+  _Float16* y;
+  const uint32_t* x32;   // the attention output row (fp16 pairs), written by this launch
+  int* done;
+  int* consumed;
+  int* err;
+  int target, nblk, has_bias;
+  int N, Kt, G, tpw;
+  uint32_t cmagic;
+};
+
+template <int BITS, int GPT, int ZM>
+__device__ __forceinline__ void oproj_body(const OArgs& O, const int nt) {
+  __shared__ __attribute__((aligned(16))) float ored[kTileN][kWaves];
+  __shared__ __attribute__((aligned(16))) uint32_t oxs[kWaves][64];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, n_in = lane & 15;
+  const uint32_t* qw = O.qw + (int64_t)nt * O.Kt * (64 * BITS) + lane * BITS;
+  const uint32_t* sz = O.qsz + (int64_t)nt * O.G * kTileN + n_in;
+  const int ktl = wave + kWaves * (O.tpw - 1);  // the wave's last k-tile: w, w + 4, ...
+  auto kt_of = [&](int i) { return min(wave + kWaves * i, ktl); };
+  auto group_of_tile = [&](int kt) {
+    return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * O.cmagic) >> 31) : kt * GPT;
+  };
+  // every weight tile of the wave in flight now, while the attention runs
+  WTile<BITS, GPT> wt[kOTpw];
+#pragma unroll
+  for (int i = 0; i < kOTpw; ++i) wt[i].pc = load_piece_nt<BITS>(qw + kt_of(i) * (64 * BITS));
+#pragma unroll
+  for (int i = 0; i < kOTpw; ++i) {
+    const int g0 = group_of_tile(kt_of(i));
+#pragma unroll
+    for (int s = 0; s < GPT; ++s) wt[i].sz[s] = sz[(g0 + s) * kTileN];
+  }
+  const int64_t orow = min((int64_t)nt * kTileN + n_in, (int64_t)O.N - 1);
+  const _Float16 ob = O.bias[orow], ores = O.res[orow];
+
+  // wait for the attention rows (one lane polls; the block meets at the barrier)
+  if (tid == 0) {
+    const int* d = O.done + 32 * (blockIdx.x % kDoneReplicas);
+    int it = 0;
+    while (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < O.target) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++it > (1 << 22)) {  // ~0.1 s: give up loudly (error word), never hang
+        __hip_atomic_store(O.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    // the last block past its wait rearms the counters for the next launch
+    if (__hip_atomic_fetch_add(O.consumed, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        O.nblk - 1) {
+      for (int r = 0; r < kDoneReplicas; ++r)
+        __hip_atomic_store(O.done + 32 * r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(O.consumed, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+
+  // the wave's x words (write-through by the attention blocks: sc1 loads)
+  uint32_t xw[kOTpw];
+#pragma unroll
+  for (int i = 0; i < kOTpw; ++i)
+    xw[i] = __hip_atomic_load(O.x32 + kt_of(i) * 64 + lane, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+  const Magics mg = make_magics<BITS>();
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  uint32_t* slot = &oxs[wave][0];
+#pragma unroll
+  for (int i = 0; i < kOTpw; ++i) {
+    XRaw<1> xr;
+    xr.w[0] = i < O.tpw ? xw[i] : 0u;  // slots past the wave's tiles: x zeroed
+    h8 xa[4];
+    park_x<1>(xa, xr, slot, lane, n_in);
+    auto step = [&](auto S_) {
+      constexpr int S = decltype(S_)::value;
+      uint32_t vv[4];
+      const GroupQ gq = make_group_w<BITS, ZM>(wt[i].sz[S * GPT / 4]);
+      dequant_step<BITS, ZM, S>(wt[i].pc, mg, gq, vv);
+      const h8 bb = __builtin_bit_cast(h8, make_uint4(vv[0], vv[1], vv[2], vv[3]));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+  }
+  if (lane < kTileN) ored[lane][wave] = acc[0];
+  __syncthreads();
+  if (tid < kTileN && (int64_t)nt * kTileN + tid < O.N) {
+    float t = (ored[tid][0] + ored[tid][1]) + (ored[tid][2] + ored[tid][3]);
+    if (O.has_bias) t += (float)ob;
+    t = (float)(_Float16)t;  // F.linear's fp16 output
+    O.y[(int64_t)nt * kTileN + tid] = (_Float16)((float)ores + t);
+  }
+}
+
+template <int GRP, int BITS, int GPT, int ZM>
+__global__ __launch_bounds__(kThreads) void attn_o_kernel(const AttnArgs A, const OArgs O) {
+  const int na = A.Hkv * A.S;  // attention blocks (batch 1) first
+  if ((int)blockIdx.x < na) {
+    attn_decode_body<GRP, true>(A, blockIdx.x / A.S, blockIdx.x % A.S);
+    return;
+  }
+  oproj_body<BITS, GPT, ZM>(O, blockIdx.x - na);
+}
+
+bool attn_o_ok(int Hq, int Hkv, int64_t L, int64_t N, int bits, int group, int flags) {
+  if (Hq <= 0 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > kMaxGroup || L < 1 || L > kMaxL || N < 1 ||
+      N > (1 << 26) || !(bits == 2 || bits == 3 || bits == 4 || bits == 8))
+    return false;
+  const int grp = Hq / Hkv;
+  if (!(grp == 1 || grp == 2 || grp == 4 || grp == 8)) return false;
+  const int64_t K = (int64_t)Hq * kD;
+  // o_proj: 4 waves x <= 8 k-tiles, whole-tile groups, narrow or fp16 zeros
+  return Hq % kWaves == 0 && Hq / kWaves <= kOTpw && group % kTileK == 0 && K % group == 0 &&
+         zero_mode(flags) != kZWide;
+}
+
+int64_t attn_o_ws_bytes(int Hq, int Hkv, int64_t L) {
+  const int64_t x_off = (kWsCounters + 4 * (int64_t)Hkv + 255) / 256 * 256;
+  const int64_t p_off = (x_off + 2 * (int64_t)Hq * kD + 255) / 256 * 256;
+  return p_off + std::max<int64_t>(0, qlin_attn_decode_partials_bytes(1, Hq, Hkv, L));
+}
+
+}  // namespace
+
+extern "C" int qlin_attn_decode_o_supported(int Hq, int Hkv, int64_t L, int64_t N, int bits,
+                                            int group, int flags) {
+  return attn_o_ok(Hq, Hkv, L, N, bits, group, flags) ? 1 : 0;
+}
+
+extern "C" int64_t qlin_attn_decode_o_workspace_bytes(int Hq, int Hkv, int64_t L) {
+  if (Hq <= 0 || Hkv <= 0 || Hq % Hkv || L < 1 || L > kMaxL) return -1;
+  return attn_o_ws_bytes(Hq, Hkv, L);
+}
+
+extern "C" int qlin_attn_decode_o_f16(
+    const uint16_t* q, int64_t q_row_stride, const uint16_t* k, int64_t k_row_stride,
+    const uint16_t* v, int64_t v_row_stride, const float* cos_cache, const float* sin_cache,
+    int64_t cache_rows, const int64_t* position_ids, uint16_t* k_cache, uint16_t* v_cache,
+    int64_t kv_head_stride, const uint16_t* mask, int Hq, int Hkv, int64_t L, int D,
+    float scale_div, const uint32_t* qweight, const uint32_t* qsz, int flags, int bits, int group,
+    const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t N, void* workspace,
+    int64_t workspace_bytes, void* stream) {
+  if (!q || !k || !v || !cos_cache || !sin_cache || !position_ids || !k_cache || !v_cache ||
+      !qweight || !qsz || !residual || !y || !workspace || D != kD ||
+      !attn_o_ok(Hq, Hkv, L, N, bits, group, flags) ||
+      workspace_bytes < attn_o_ws_bytes(Hq, Hkv, L) || ((uintptr_t)workspace & 255) ||
+      q_row_stride < (int64_t)Hq * kD || k_row_stride < (int64_t)Hkv * kD ||
+      v_row_stride < (int64_t)Hkv * kD || cache_rows <= 0 || kv_head_stride < L * kD ||
+      kv_head_stride % 8)
+    return QLIN_EINVAL;
+  const Split sp = choose_split(1, Hkv, L);
+  char* ws = (char*)workspace;
+  const int64_t x_off = (kWsCounters + 4 * (int64_t)Hkv + 255) / 256 * 256;
+  const int64_t p_off = (x_off + 2 * (int64_t)Hq * kD + 255) / 256 * 256;
+  const int grp = Hq / Hkv;
+  float* part_o = sp.S > 1 ? (float*)(ws + p_off) : nullptr;
+  float* part_ml = sp.S > 1 ? part_o + (int64_t)Hkv * sp.S * grp * kD : nullptr;
+  const RopeIn ri{(const _Float16*)q, q_row_stride, (const _Float16*)k, k_row_stride,
+                  (const _Float16*)v, v_row_stride, cos_cache, sin_cache, cache_rows,
+                  position_ids, 0, (_Float16*)k_cache, (_Float16*)v_cache};
+  const AttnArgs A{nullptr, (const _Float16*)k_cache, (const _Float16*)v_cache,
+                   (const _Float16*)mask, ws + x_off, 1, Hq, Hkv, (int)L, kv_head_stride,
+                   sp.chunk, sp.S, scale_div, (int*)(ws + kWsCounters), part_o, part_ml, ri,
+                   (int*)(ws + kWsDone)};
+  OArgs O;
+  O.qw = qweight;
+  O.qsz = qsz;
+  O.has_bias = bias != nullptr;
+  O.bias = (const _Float16*)(bias ? bias : residual);
+  O.res = (const _Float16*)residual;
+  O.y = (_Float16*)y;
+  O.x32 = (const uint32_t*)(ws + x_off);
+  O.done = (int*)(ws + kWsDone);
+  O.consumed = (int*)(ws + kWsConsumed);
+  O.err = (int*)(ws + kWsErr);
+  O.target = Hkv;
+  O.N = (int)N;
+  O.Kt = Hq;
+  O.G = (int)((int64_t)Hq * kD / group);
+  O.tpw = Hq / kWaves;
+  const uint64_t c = (uint64_t)(group / kTileK);
+  O.cmagic = (uint32_t)(((1ull << 31) + c - 1) / c);
+  const int nt = (int)((N + kTileN - 1) / kTileN);
+  O.nblk = nt;
+  const dim3 grid((unsigned)(Hkv * sp.S + nt));
+  hipStream_t st = (hipStream_t)stream;
+  const int zm = zero_mode(flags);
+#define QLIN_AO(G, B, Z) hipLaunchKernelGGL((attn_o_kernel<G, B, 1, Z>), grid, dim3(kThreads), 0, st, A, O)
+#define QLIN_AOZ(G, B)                 \
+  if (zm == kZFloat) QLIN_AO(G, B, kZFloat); \
+  else QLIN_AO(G, B, kZNarrow)
+#define QLIN_AOB(G)                    \
+  switch (bits) {                      \
+    case 2: QLIN_AOZ(G, 2); break;     \
+    case 3: QLIN_AOZ(G, 3); break;     \
+    case 4: QLIN_AOZ(G, 4); break;     \
+    default: QLIN_AOZ(G, 8); break;    \
+  }
+  switch (grp) {
+    case 1: QLIN_AOB(1); break;
+    case 2: QLIN_AOB(2); break;
+    case 4: QLIN_AOB(4); break;
+    default: QLIN_AOB(8); break;
+  }
+#undef QLIN_AOB
+#undef QLIN_AOZ
+#undef QLIN_AO
+  return (int)hipGetLastError();
 }
