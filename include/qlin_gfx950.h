@@ -284,33 +284,6 @@ int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_
                           float scale_div, float* partials, int32_t* counters, void* stream);
 
 /*
- * qlin_attn_decode_rope (fp16 output) + o_proj with the residual epilogue in ONE launch, batch 1:
- * y = RN16(residual + RN16(o_proj(attn) + bias)) (models/int_llama_layer.py:174 and :249 of the
- * reference: self.o_proj(attn_output), hidden_states = residual + hidden_states).  o_proj is the
- * packed [N, Hq * D] matrix (qweight / qsz / flags as qlin_gemv_f16, group a multiple of 128,
- * narrow or fp16 zeros), bias fp16 [N] or NULL, residual / y fp16 [N].  The o_proj blocks of the
- * grid load their weight tiles while the attention blocks run and wait on completion counters
- * in the workspace: qlin_attn_decode_o_workspace_bytes(Hq, Hkv, L) bytes, 256-B aligned,
- * zero-filled before its first use and left with its counters zero by every call (one workspace
- * per stream; graph replays included).  The int32 at byte 1152 of the workspace becomes nonzero
- * if a launch ever gave up waiting (bounded wait, ~0.1 s: its output is then wrong).
- * qlin_attn_decode_o_supported(): 1 when the heads / o_proj shape / bits / group / zero mode can
- * run fused (Hq a multiple of 4, Hq <= 32, GQA group 1/2/4/8, L <= 4096), else 0.
- */
-int qlin_attn_decode_o_supported(int Hq, int Hkv, int64_t L, int64_t N, int bits, int group,
-                                 int flags);
-int64_t qlin_attn_decode_o_workspace_bytes(int Hq, int Hkv, int64_t L);
-int qlin_attn_decode_o_f16(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
-                           int64_t k_row_stride, const uint16_t* v, int64_t v_row_stride,
-                           const float* cos_cache, const float* sin_cache, int64_t cache_rows,
-                           const int64_t* position_ids, uint16_t* k_cache, uint16_t* v_cache,
-                           int64_t kv_head_stride, const uint16_t* mask, int Hq, int Hkv,
-                           int64_t L, int D, float scale_div, const uint32_t* qweight,
-                           const uint32_t* qsz, int flags, int bits, int group,
-                           const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t N,
-                           void* workspace, int64_t workspace_bytes, void* stream);
-
-/*
  * Fused prefill attention (many query tokens per sequence): the same attention core as
  * qlin_attn_decode — repeat_kv, fp32 QK^T, / sqrt(head_dim) (as torch: x the fp32 reciprocal),
  * + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV (models/int_llama_layer.py:137-165 of

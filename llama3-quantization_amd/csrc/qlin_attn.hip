@@ -15,9 +15,16 @@
 // graph-replayable with no memset.
 //
 // Latency: decode attention at batch 1 is a chain of dependent memory round trips, not a bandwidth
-// problem, so a block issues the K rows, V rows and mask of its first 64 positions before it waits
-// on q, and the merge reads the partials with all 256 threads (one coalesced 256-B row per wave
-// and load).
+// problem.  A block issues the q side first (ROPE: the q / k / v rows of the step and the cos /
+// sin rows at the guessed position L - 1, the new token's cache row; a padded sequence whose
+// position id differs redoes RoPE on its own path), then the K rows, V rows and mask of its first
+// 64 positions, so its first wait covers the q side only and no load waits on another one (the
+// position id -> cos / sin chain cost 1 us: profiles/r4_attn_decode.txt); mask values are loaded
+// unconditionally (a load under a branch gets its own full wait).  The merge reads the partials
+// with all 256 threads (one coalesced 256-B row per wave and load).
+// One 1024-thread block per (b, kv head) streaming all 513 rows (no merge) and 256-row blocks
+// were both slower: one CU takes ~4-6 us to land 256 KB of cold K / V, more than the merge chain
+// (tools/dev/cu_bw.hip; profiles/r4_attn_decode.txt).
 //
 // Cross-block hand-off: the partials are written and read with agent-scope (sc1) accesses and the
 // writer drains its stores (vmcnt) before the block barrier and the counter atomic.  A device-scope
@@ -28,9 +35,7 @@
 // and sums run in a different order than hipBLASLt's bmm and the softmax is merged across chunks
 // (exp(m_c - M) rescaling), so results agree with the reference to fp32 rounding, not bit for bit.
 #include "qlin_common.h"  // QLIN_OK / QLIN_EINVAL
-#include "qlin_gemv_tile.h"  // packed-tile helpers of the fused o_proj (attn_o_kernel)
 
-#include <algorithm>
 #include "../../include/qlin_gfx950.h"
 
 namespace {
@@ -127,9 +132,23 @@ struct AttnArgs {
   float* part_o;
   float* part_ml;
   RopeIn ri;
-  int* done;  // attn_o: kDoneReplicas completion counters, each += 1 per merged (b, kv head)
+#ifdef ATTN_STAMP
+  uint64_t* stamps;
+#endif
 };
-constexpr int kDoneReplicas = 8;  // one 128-B line each (32 ints apart)
+
+// dev build only (tools/dev/attn_stamps.py): s_memrealtime (100 MHz) per block [block][8] at
+// 0 start, 1 q ready, 2 scores (K landed), 3 P V (V landed), 4 partials counted, 5 merge inputs
+// loaded, 6 output stored
+#ifdef ATTN_STAMP
+inline uint64_t* g_attn_stamps = nullptr;
+#define AT_STAMP(P, k)                                                                          \
+  if ((P).stamps && threadIdx.x == 0)                                                          \
+  (P).stamps[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] =                      \
+      __builtin_amdgcn_s_memrealtime()
+#else
+#define AT_STAMP(P, k)
+#endif
 
 template <int GRP, bool ROPE = false>
 __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh, const int split) {
@@ -155,17 +174,56 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   __shared__ float ml_l[kMaxSplit][GRP];   // merge: chunk sums
   __shared__ int last;
 
+  AT_STAMP(A, 0);
   const int b = bh / Hkv, hk = bh % Hkv;  // bh = b * Hkv + kv head
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int sub = tid & 7, tl = tid >> 3;  // score passes: 8 lanes x 16 dims per K row
   const int t0 = split * chunk;
   const int n = min(chunk, L - t0);  // positions in this chunk (>= 1)
+  const bool has_new = ROPE && split == S - 1;  // this block's chunk holds the new row L - 1
+  constexpr int half = kD / 2;
+  constexpr int QE = (GRP * kD + kThreads - 1) / kThreads;  // q elements per thread
+
+  // ---- the q side first (its wait then does not wait for the K / V loads behind it) ----
+  // ROPE: q / k / v rows of the step, the position id and the cos / sin rows at the guessed
+  // position L - 1 (the new token's cache row; a padded sequence's position id differs and
+  // takes the reload path below), so no load waits on another one
+  float q_x[QE], q_rx[QE], c_q[QE], s_q[QE];
+  float k_x = 0.f, k_rx = 0.f;
+  _Float16 v_x = 0;
+  int64_t p_guess = 0, p_raw = 0;
+  const int dn = tid & (kD - 1), dp = dn < half ? dn + half : dn - half;
+  if constexpr (ROPE) {
+    p_guess = ri.pos ? min((int64_t)L - 1, ri.cache_rows - 1) : 0;
+    if (ri.pos) p_raw = ri.pos[(int64_t)b * ri.pos_bs];  // scalar load (lgkmcnt)
+#pragma unroll
+    for (int e = 0; e < QE; ++e) {
+      const int i = min(tid + kThreads * e, GRP * kD - 1);
+      const int g = i / kD, d = i % kD;
+      const _Float16* qr = ri.q16 + (int64_t)b * ri.q_rs + (int64_t)(hk * GRP + g) * kD;
+      q_x[e] = (float)qr[d];
+      q_rx[e] = (float)qr[d < half ? d + half : d - half];
+      c_q[e] = ri.cosc[p_guess * kD + d];
+      s_q[e] = ri.sinc[p_guess * kD + d];
+    }
+    const _Float16* kr = ri.k16 + (int64_t)b * ri.k_rs + (int64_t)hk * kD;
+    k_x = (float)kr[dn];
+    k_rx = (float)kr[dp];
+    v_x = ri.v16[(int64_t)b * ri.v_rs + (int64_t)hk * kD + dn];
+  } else {
+    const float* qb = q + ((int64_t)b * Hq + (int64_t)hk * GRP) * kD;
+#pragma unroll
+    for (int e = 0; e < QE; ++e) q_x[e] = qb[min(tid + kThreads * e, GRP * kD - 1)];
+  }
+  asm volatile("" ::: "memory");  // the K / V loads are issued after the q side
 
   // cache rows of (b, kv head) bh start at bh * kv_hs (a KV cache with spare rows: kv_hs > L * kD)
   const _Float16* kb = k + (int64_t)bh * kv_hs + (int64_t)t0 * kD;
   const uint32_t* vb =
       reinterpret_cast<const uint32_t*>(v + (int64_t)bh * kv_hs + (int64_t)t0 * kD) + lane;
-  const _Float16* mb = mask ? mask + (int64_t)b * L + t0 : nullptr;
+  // mask values are loaded unconditionally (from kb when there is no mask) and selected: a load
+  // under a branch is followed by its own full wait
+  const _Float16* mb = mask ? mask + (int64_t)b * L + t0 : kb;
 
   // issue the first pass's K rows, V words and mask before anything waits
   u32x4 kw[2][2];
@@ -177,7 +235,8 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
       const u32x4* kr = reinterpret_cast<const u32x4*>(kb + (int64_t)t * kD + 16 * sub);
       kw[u][0] = __builtin_nontemporal_load(kr);
       kw[u][1] = __builtin_nontemporal_load(kr + 1);
-      mv[u] = mb ? (float)mb[t] : 0.f;
+      const float m = (float)mb[t];
+      mv[u] = mask ? m : 0.f;
     }
   };
   uint32_t vw[kSub / kWaves];  // PV: lane = dim pair, wave = every 4th position
@@ -190,44 +249,53 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   };
   load_k(0);
   load_v(0);
+  asm volatile("" ::: "memory");
 
-  const bool has_new = ROPE && split == S - 1;  // this block's chunk holds the new row L - 1
   if constexpr (ROPE) {
 #pragma clang fp contract(off)
-    // pos NULL: cosc / sinc already are the step's rows (qlin_rmsnorm_linear_ep_f16 rope_out)
-    const int64_t p =
-        ri.pos ? min(max(ri.pos[(int64_t)b * ri.pos_bs], (int64_t)0), ri.cache_rows - 1) : 0;
-    const float* cr = ri.cosc + p * kD;
-    const float* sr = ri.sinc + p * kD;
-    constexpr int half = kD / 2;
-    for (int i = tid; i < GRP * kD; i += kThreads) {
-      const int g = i / kD, d = i % kD;
-      const _Float16* qr = ri.q16 + (int64_t)b * ri.q_rs + (int64_t)(hk * GRP + g) * kD;
-      const float c = (float)(_Float16)cr[d], sn = (float)(_Float16)sr[d];
-      const float x = (float)qr[d];
-      const float rx = d < half ? -(float)qr[d + half] : (float)qr[d - half];
-      qs[g][d] = x * c + rx * sn;  // fp32, each op rounded once (qlin_rope_f16)
-    }
-    if (has_new && tid < kD) {
-      const int d = tid;
-      const _Float16* kr = ri.k16 + (int64_t)b * ri.k_rs + (int64_t)hk * kD;
-      const float c = (float)(_Float16)cr[d], sn = (float)(_Float16)sr[d];
-      const float x = (float)kr[d];
-      const float rx = d < half ? -(float)kr[d + half] : (float)kr[d - half];
-      const float a0 = (float)(_Float16)(x * c), b0 = (float)(_Float16)(rx * sn);
-      const _Float16 kn = (_Float16)(a0 + b0);  // fp16 ops, as the reference's k path
-      const _Float16 vn = ri.v16[(int64_t)b * ri.v_rs + (int64_t)hk * kD + d];
-      knew[d] = kn;
-      vnew[d] = vn;
-      const int64_t row = (int64_t)bh * kv_hs + (int64_t)(L - 1) * kD + d;
-      ri.kc[row] = kn;  // the cache row, for the following steps
-      ri.vc[row] = vn;
+    auto rope_apply = [&](const float* cr, const float* sr) {
+#pragma unroll
+      for (int e = 0; e < QE; ++e) {
+        const int i = tid + kThreads * e;
+        const int g = min(i, GRP * kD - 1) / kD, d = min(i, GRP * kD - 1) % kD;
+        const float c = (float)(_Float16)cr[e], sn = (float)(_Float16)sr[e];
+        const float rx = d < half ? -q_rx[e] : q_rx[e];
+        if (i < GRP * kD) qs[g][d] = q_x[e] * c + rx * sn;  // fp32, each op rounded once
+      }
+      if (has_new && tid < kD) {
+        // thread tid < 128 rotates k dim tid: q element tid (g = 0, d = tid) has its cos / sin
+        const float c = (float)(_Float16)cr[0], sn = (float)(_Float16)sr[0];
+        const float rx = tid < half ? -k_rx : k_rx;
+        const float a0 = (float)(_Float16)(k_x * c), b0 = (float)(_Float16)(rx * sn);
+        const _Float16 kn = (_Float16)(a0 + b0);  // fp16 ops, as the reference's k path
+        knew[tid] = kn;
+        vnew[tid] = v_x;
+        const int64_t row = (int64_t)bh * kv_hs + (int64_t)(L - 1) * kD + tid;
+        ri.kc[row] = kn;  // the cache row, for the following steps
+        ri.vc[row] = v_x;
+      }
+    };
+    rope_apply(c_q, s_q);
+    const int64_t p_true = ri.pos ? min(max(p_raw, (int64_t)0), ri.cache_rows - 1) : 0;
+    if (p_true != p_guess) {  // block-uniform; its own path, so the common one waits early
+      float c2[QE], s2[QE];
+#pragma unroll
+      for (int e = 0; e < QE; ++e) {
+        const int d = min(tid + kThreads * e, GRP * kD - 1) % kD;
+        c2[e] = ri.cosc[p_true * kD + d];
+        s2[e] = ri.sinc[p_true * kD + d];
+      }
+      rope_apply(c2, s2);
     }
   } else {
-    const float* qb = q + ((int64_t)b * Hq + (int64_t)hk * GRP) * kD;
-    for (int i = tid; i < GRP * kD; i += kThreads) qs[i / kD][i % kD] = qb[i];
+#pragma unroll
+    for (int e = 0; e < QE; ++e) {
+      const int i = tid + kThreads * e;
+      if (i < GRP * kD) qs[i / kD][i % kD] = q_x[e];
+    }
   }
   __syncthreads();
+  AT_STAMP(A, 1);
 
   // scores (the next pass's K rows are in flight while this pass computes)
   for (int tb = 0; tb < n; tb += kSub) {
@@ -280,6 +348,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     }
   }
   __syncthreads();
+  AT_STAMP(A, 2);
 
   // chunk softmax statistics: wave w owns query heads w, w + 4 (wave-level reductions only)
   for (int g = wave; g < GRP; g += kWaves) {
@@ -335,6 +404,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     }
   }
   __syncthreads();
+  AT_STAMP(A, 3);
 
   const int64_t qh0 = (int64_t)b * Hq + (int64_t)hk * GRP;  // first query head of the group
   // output row of the group: fp32, or rounded once to fp16 (== the reference's .to(fp16))
@@ -342,26 +412,10 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     if (out_f16) reinterpret_cast<_Float16*>(out)[qh0 * kD + o] = (_Float16)val;
     else reinterpret_cast<float*>(out)[qh0 * kD + o] = val;
   };
-  // attn_o (done != null, fp16 out): the output row stored write-through (sc1) as fp16 pairs,
-  // drained, then counted into every completion replica by one lane (the o_proj blocks of the
-  // same launch poll them, then read the row with sc1 loads; MI355X_MICROARCH.md hand-off table)
   auto put_all = [&]() {
-    if (A.done) {
-      uint32_t* o32 = reinterpret_cast<uint32_t*>(reinterpret_cast<_Float16*>(out) + qh0 * kD);
-      for (int o = 2 * tid; o < GRP * kD; o += 2 * kThreads) {
-        const float v0 = (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD];
-        const float v1 = (po[0][o + 1] + po[1][o + 1] + po[2][o + 1] + po[3][o + 1]) / cl[o / kD];
-        __hip_atomic_store(o32 + o / 2, qlin::as_u32(qlin::h2{(_Float16)v0, (_Float16)v1}),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid < kDoneReplicas)
-        __hip_atomic_fetch_add(A.done + 32 * tid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
     for (int o = tid; o < GRP * kD; o += kThreads)
       put(o, (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD]);
+    AT_STAMP(A, 6);
   };
   if (S == 1) {
     put_all();
@@ -386,6 +440,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     last = (__hip_atomic_fetch_add(&counters[bh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
             S - 1);
   __syncthreads();
+  AT_STAMP(A, 4);
   if (!last) return;
 #if ATTN_FENCE_MODE != 0
   __threadfence();
@@ -424,6 +479,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     if (lane == 0) cl[g] = den;
   }
   __syncthreads();
+  AT_STAMP(A, 5);
   // weighted sum of the S partial rows: wave w takes rows s = w, w + 4, ...; lane owns floats
   // o = lane + 64 j of the GRP x 128 row (one coalesced 256-B load per wave and j)
   {
@@ -477,9 +533,12 @@ int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const ui
                   const Split& sp, hipStream_t st, const RopeIn& ri) {
   const dim3 grid((unsigned)(B * Hkv), (unsigned)sp.S);
   const int grp = Hq / Hkv;
-  const AttnArgs A{q, (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,
+  AttnArgs A{q, (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,
                    out_dtype == QLIN_F16, Hq, Hkv, (int)L, kv_hs, sp.chunk, sp.S, scale_div,
-                   (int*)counters, part_o, part_ml, ri, nullptr};
+                   (int*)counters, part_o, part_ml, ri};
+#ifdef ATTN_STAMP
+  A.stamps = g_attn_stamps;
+#endif
 #define QLIN_A(G, R) \
   hipLaunchKernelGGL((attn_decode_kernel<G, R>), grid, dim3(kThreads), 0, st, A)
 #define QLIN_AR(G)                \
@@ -499,6 +558,10 @@ int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const ui
 }
 
 }  // namespace
+
+#ifdef ATTN_STAMP
+extern "C" void qlin_dev_attn_stamps(uint64_t* p) { g_attn_stamps = p; }
+#endif
 
 extern "C" int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L) {
   if (B < 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv || L <= 0 || L > kMaxL) return -1;
@@ -594,246 +657,3 @@ extern "C" int qlin_attn_decode_splits(int64_t B, int Hkv, int64_t L) {
   return choose_split(B, Hkv, L).S;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Decode attention + o_proj (+ residual) in ONE launch (qlin_attn_decode_o_f16, batch 1).
-//
-// The reference's o_proj(attn_output) and the decoder layer's residual add
-// (models/int_llama_layer.py:174, :249) read the attention output, a grid-wide dependency: as two
-// launches the o_proj GEMV pays a kernel boundary and then its weights' HBM round trip only after
-// the attention has finished.  Here the grid holds the attention blocks (split-L, as
-// qlin_attn_decode_rope; dispatched first: lower block indices) and one o_proj block per 16-row
-// tile of o_proj; an o_proj block issues all its packed weight tiles at once (the whole 8.8 MB of
-// a 4096 x 4096 int4 o_proj is in flight while the attention computes), then waits for the
-// attention: every merged (b, kv head) output row is stored write-through (sc1) and counted into
-// kDoneReplicas completion counters; one lane of each o_proj block polls its replica with sc1
-// loads (s_sleep between polls), then the block reads the attention row with sc1 loads and
-// finishes the GEMV: exact W_dq, one MFMA chain per wave, the 4 wave partials added in a fixed
-// order, F.linear's fp16 output, + residual (one fp16 rounding).  The last o_proj block to pass
-// its wait resets the counters (graph-replayable, no memset).  A wait is bounded: after
-// ~0.1 s it sets the workspace error word and proceeds (wrong output, no hang).
-// Deadlock freedom: the attention blocks never wait for o_proj blocks and are dispatched first.
-// ---------------------------------------------------------------------------------------------
-namespace {
-
-constexpr int kOTpw = 8;           // o_proj k-tiles per wave (4 waves: K <= 32 x 128)
-constexpr int kWsDone = 0;         // workspace offsets (bytes)
-constexpr int kWsConsumed = 1024;
-constexpr int kWsErr = 1152;
-constexpr int kWsCounters = 1280;  // attention merge counters, int32 [Hkv]
-
-struct OArgs {
-  const uint32_t* qw;
-  const uint32_t* qsz;
-  const _Float16* bias;  // never null (points at residual when absent; has_bias says)
-  const _Float16* res;
-  _Float16* y;
-  const uint32_t* x32;   // the attention output row (fp16 pairs), written by this launch
-  int* done;
-  int* consumed;
-  int* err;
-  int target, nblk, has_bias;
-  int N, Kt, G, tpw;
-  uint32_t cmagic;
-};
-
-template <int BITS, int GPT, int ZM>
-__device__ __forceinline__ void oproj_body(const OArgs& O, const int nt) {
-  __shared__ __attribute__((aligned(16))) float ored[kTileN][kWaves];
-  __shared__ __attribute__((aligned(16))) uint32_t oxs[kWaves][64];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63, n_in = lane & 15;
-  const uint32_t* qw = O.qw + (int64_t)nt * O.Kt * (64 * BITS) + lane * BITS;
-  const uint32_t* sz = O.qsz + (int64_t)nt * O.G * kTileN + n_in;
-  const int ktl = wave + kWaves * (O.tpw - 1);  // the wave's last k-tile: w, w + 4, ...
-  auto kt_of = [&](int i) { return min(wave + kWaves * i, ktl); };
-  auto group_of_tile = [&](int kt) {
-    return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * O.cmagic) >> 31) : kt * GPT;
-  };
-  // every weight tile of the wave in flight now, while the attention runs
-  WTile<BITS, GPT> wt[kOTpw];
-#pragma unroll
-  for (int i = 0; i < kOTpw; ++i) wt[i].pc = load_piece_nt<BITS>(qw + kt_of(i) * (64 * BITS));
-#pragma unroll
-  for (int i = 0; i < kOTpw; ++i) {
-    const int g0 = group_of_tile(kt_of(i));
-#pragma unroll
-    for (int s = 0; s < GPT; ++s) wt[i].sz[s] = sz[(g0 + s) * kTileN];
-  }
-  const int64_t orow = min((int64_t)nt * kTileN + n_in, (int64_t)O.N - 1);
-  const _Float16 ob = O.bias[orow], ores = O.res[orow];
-
-  // wait for the attention rows (one lane polls; the block meets at the barrier)
-  if (tid == 0) {
-    const int* d = O.done + 32 * (blockIdx.x % kDoneReplicas);
-    int it = 0;
-    while (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < O.target) {
-      __builtin_amdgcn_s_sleep(4);
-      if (++it > (1 << 22)) {  // ~0.1 s: give up loudly (error word), never hang
-        __hip_atomic_store(O.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    // the last block past its wait rearms the counters for the next launch
-    if (__hip_atomic_fetch_add(O.consumed, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        O.nblk - 1) {
-      for (int r = 0; r < kDoneReplicas; ++r)
-        __hip_atomic_store(O.done + 32 * r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(O.consumed, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-
-  // the wave's x words (write-through by the attention blocks: sc1 loads)
-  uint32_t xw[kOTpw];
-#pragma unroll
-  for (int i = 0; i < kOTpw; ++i)
-    xw[i] = __hip_atomic_load(O.x32 + kt_of(i) * 64 + lane, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-  const Magics mg = make_magics<BITS>();
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  uint32_t* slot = &oxs[wave][0];
-#pragma unroll
-  for (int i = 0; i < kOTpw; ++i) {
-    XRaw<1> xr;
-    xr.w[0] = i < O.tpw ? xw[i] : 0u;  // slots past the wave's tiles: x zeroed
-    h8 xa[4];
-    park_x<1>(xa, xr, slot, lane, n_in);
-    auto step = [&](auto S_) {
-      constexpr int S = decltype(S_)::value;
-      uint32_t vv[4];
-      const GroupQ gq = make_group_w<BITS, ZM>(wt[i].sz[S * GPT / 4]);
-      dequant_step<BITS, ZM, S>(wt[i].pc, mg, gq, vv);
-      const h8 bb = __builtin_bit_cast(h8, make_uint4(vv[0], vv[1], vv[2], vv[3]));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
-    };
-    step(std::integral_constant<int, 0>{});
-    step(std::integral_constant<int, 1>{});
-    step(std::integral_constant<int, 2>{});
-    step(std::integral_constant<int, 3>{});
-  }
-  if (lane < kTileN) ored[lane][wave] = acc[0];
-  __syncthreads();
-  if (tid < kTileN && (int64_t)nt * kTileN + tid < O.N) {
-    float t = (ored[tid][0] + ored[tid][1]) + (ored[tid][2] + ored[tid][3]);
-    if (O.has_bias) t += (float)ob;
-    t = (float)(_Float16)t;  // F.linear's fp16 output
-    O.y[(int64_t)nt * kTileN + tid] = (_Float16)((float)ores + t);
-  }
-}
-
-template <int GRP, int BITS, int GPT, int ZM>
-__global__ __launch_bounds__(kThreads) void attn_o_kernel(const AttnArgs A, const OArgs O) {
-  const int na = A.Hkv * A.S;  // attention blocks (batch 1) first
-  if ((int)blockIdx.x < na) {
-    attn_decode_body<GRP, true>(A, blockIdx.x / A.S, blockIdx.x % A.S);
-    return;
-  }
-  oproj_body<BITS, GPT, ZM>(O, blockIdx.x - na);
-}
-
-bool attn_o_ok(int Hq, int Hkv, int64_t L, int64_t N, int bits, int group, int flags) {
-  if (Hq <= 0 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > kMaxGroup || L < 1 || L > kMaxL || N < 1 ||
-      N > (1 << 26) || !(bits == 2 || bits == 3 || bits == 4 || bits == 8))
-    return false;
-  const int grp = Hq / Hkv;
-  if (!(grp == 1 || grp == 2 || grp == 4 || grp == 8)) return false;
-  const int64_t K = (int64_t)Hq * kD;
-  // o_proj: 4 waves x <= 8 k-tiles, whole-tile groups, narrow or fp16 zeros
-  return Hq % kWaves == 0 && Hq / kWaves <= kOTpw && group % kTileK == 0 && K % group == 0 &&
-         zero_mode(flags) != kZWide;
-}
-
-int64_t attn_o_ws_bytes(int Hq, int Hkv, int64_t L) {
-  const int64_t x_off = (kWsCounters + 4 * (int64_t)Hkv + 255) / 256 * 256;
-  const int64_t p_off = (x_off + 2 * (int64_t)Hq * kD + 255) / 256 * 256;
-  return p_off + std::max<int64_t>(0, qlin_attn_decode_partials_bytes(1, Hq, Hkv, L));
-}
-
-}  // namespace
-
-extern "C" int qlin_attn_decode_o_supported(int Hq, int Hkv, int64_t L, int64_t N, int bits,
-                                            int group, int flags) {
-  return attn_o_ok(Hq, Hkv, L, N, bits, group, flags) ? 1 : 0;
-}
-
-extern "C" int64_t qlin_attn_decode_o_workspace_bytes(int Hq, int Hkv, int64_t L) {
-  if (Hq <= 0 || Hkv <= 0 || Hq % Hkv || L < 1 || L > kMaxL) return -1;
-  return attn_o_ws_bytes(Hq, Hkv, L);
-}
-
-extern "C" int qlin_attn_decode_o_f16(
-    const uint16_t* q, int64_t q_row_stride, const uint16_t* k, int64_t k_row_stride,
-    const uint16_t* v, int64_t v_row_stride, const float* cos_cache, const float* sin_cache,
-    int64_t cache_rows, const int64_t* position_ids, uint16_t* k_cache, uint16_t* v_cache,
-    int64_t kv_head_stride, const uint16_t* mask, int Hq, int Hkv, int64_t L, int D,
-    float scale_div, const uint32_t* qweight, const uint32_t* qsz, int flags, int bits, int group,
-    const uint16_t* bias, const uint16_t* residual, uint16_t* y, int64_t N, void* workspace,
-    int64_t workspace_bytes, void* stream) {
-  if (!q || !k || !v || !cos_cache || !sin_cache || !position_ids || !k_cache || !v_cache ||
-      !qweight || !qsz || !residual || !y || !workspace || D != kD ||
-      !attn_o_ok(Hq, Hkv, L, N, bits, group, flags) ||
-      workspace_bytes < attn_o_ws_bytes(Hq, Hkv, L) || ((uintptr_t)workspace & 255) ||
-      q_row_stride < (int64_t)Hq * kD || k_row_stride < (int64_t)Hkv * kD ||
-      v_row_stride < (int64_t)Hkv * kD || cache_rows <= 0 || kv_head_stride < L * kD ||
-      kv_head_stride % 8)
-    return QLIN_EINVAL;
-  const Split sp = choose_split(1, Hkv, L);
-  char* ws = (char*)workspace;
-  const int64_t x_off = (kWsCounters + 4 * (int64_t)Hkv + 255) / 256 * 256;
-  const int64_t p_off = (x_off + 2 * (int64_t)Hq * kD + 255) / 256 * 256;
-  const int grp = Hq / Hkv;
-  float* part_o = sp.S > 1 ? (float*)(ws + p_off) : nullptr;
-  float* part_ml = sp.S > 1 ? part_o + (int64_t)Hkv * sp.S * grp * kD : nullptr;
-  const RopeIn ri{(const _Float16*)q, q_row_stride, (const _Float16*)k, k_row_stride,
-                  (const _Float16*)v, v_row_stride, cos_cache, sin_cache, cache_rows,
-                  position_ids, 0, (_Float16*)k_cache, (_Float16*)v_cache};
-  const AttnArgs A{nullptr, (const _Float16*)k_cache, (const _Float16*)v_cache,
-                   (const _Float16*)mask, ws + x_off, 1, Hq, Hkv, (int)L, kv_head_stride,
-                   sp.chunk, sp.S, scale_div, (int*)(ws + kWsCounters), part_o, part_ml, ri,
-                   (int*)(ws + kWsDone)};
-  OArgs O;
-  O.qw = qweight;
-  O.qsz = qsz;
-  O.has_bias = bias != nullptr;
-  O.bias = (const _Float16*)(bias ? bias : residual);
-  O.res = (const _Float16*)residual;
-  O.y = (_Float16*)y;
-  O.x32 = (const uint32_t*)(ws + x_off);
-  O.done = (int*)(ws + kWsDone);
-  O.consumed = (int*)(ws + kWsConsumed);
-  O.err = (int*)(ws + kWsErr);
-  O.target = Hkv;
-  O.N = (int)N;
-  O.Kt = Hq;
-  O.G = (int)((int64_t)Hq * kD / group);
-  O.tpw = Hq / kWaves;
-  const uint64_t c = (uint64_t)(group / kTileK);
-  O.cmagic = (uint32_t)(((1ull << 31) + c - 1) / c);
-  const int nt = (int)((N + kTileN - 1) / kTileN);
-  O.nblk = nt;
-  const dim3 grid((unsigned)(Hkv * sp.S + nt));
-  hipStream_t st = (hipStream_t)stream;
-  const int zm = zero_mode(flags);
-#define QLIN_AO(G, B, Z) hipLaunchKernelGGL((attn_o_kernel<G, B, 1, Z>), grid, dim3(kThreads), 0, st, A, O)
-#define QLIN_AOZ(G, B)                 \
-  if (zm == kZFloat) QLIN_AO(G, B, kZFloat); \
-  else QLIN_AO(G, B, kZNarrow)
-#define QLIN_AOB(G)                    \
-  switch (bits) {                      \
-    case 2: QLIN_AOZ(G, 2); break;     \
-    case 3: QLIN_AOZ(G, 3); break;     \
-    case 4: QLIN_AOZ(G, 4); break;     \
-    default: QLIN_AOZ(G, 8); break;    \
-  }
-  switch (grp) {
-    case 1: QLIN_AOB(1); break;
-    case 2: QLIN_AOB(2); break;
-    case 4: QLIN_AOB(4); break;
-    default: QLIN_AOB(8); break;
-  }
-#undef QLIN_AOB
-#undef QLIN_AOZ
-#undef QLIN_AO
-  return (int)hipGetLastError();
-}

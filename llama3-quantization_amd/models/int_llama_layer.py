@@ -297,16 +297,6 @@ class QuantLlamaAttention(nn.Module):
             self._rope32_key = key
         return self._rope32
 
-    def _attn_o_ok(self, residual, act_dtype, position_ids, mask, L):
-        """Whether the decode attention and o_proj (+ residual) run as one launch."""
-        o = self.o_proj
-        return (residual is not None and act_dtype == torch.float16 and o.packed
-                and residual.dtype == torch.float16 and residual.shape[0] == 1
-                and position_ids is not None and act_spec(o) == (0, 0)
-                and (mask is None or mask.dtype == torch.float16)
-                and qlin.attn_decode_o_supported(self.num_heads, self.num_key_value_heads, L,
-                                                 o.out_features, o.wbits, o.group, o.qflags))
-
     def _out(self, attn_output, residual):
         if residual is None:
             return self.o_proj(attn_output)
@@ -352,17 +342,6 @@ class QuantLlamaAttention(nn.Module):
             if decode:
                 # one launch: RoPE, the cache append and the decode attention
                 buf, L0 = self._cache_for(past_key_value, bsz, 1, q.device)
-                if self._attn_o_ok(residual, act_dtype, position_ids, attention_mask, L0 + 1):
-                    # ... and o_proj with the residual add, in the same launch
-                    o = self.o_proj
-                    bias = None if o.bias is None else o.bias.to(torch.float16).contiguous()
-                    out = qlin.attn_decode_o(
-                        q, k, v, cos_c, sin_c, position_ids, self.num_heads,
-                        self.num_key_value_heads, self.head_dim, buf[0], buf[1], L0,
-                        attention_mask, math.sqrt(self.head_dim), o.qweight, o.qsz,
-                        o.out_features, o.wbits, o.group, o.qflags, bias, residual.contiguous())
-                    past_key_value = (buf[0][:, :, :L0 + 1], buf[1][:, :, :L0 + 1]) if use_cache else None
-                    return out, None, past_key_value
                 attn_output = qlin.attn_decode_rope(
                     q, k, v, cos_c, sin_c, position_ids, self.num_heads, self.num_key_value_heads,
                     self.head_dim, buf[0], buf[1], L0, attention_mask, math.sqrt(self.head_dim),

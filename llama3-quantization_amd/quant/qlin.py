@@ -70,11 +70,6 @@ SIGNATURES = {
                           _p],
                          _i),
     "qlin_attn_decode_splits": ([_l, _i, _l], _i),
-    "qlin_attn_decode_o_supported": ([_i, _i, _l, _l, _i, _i, _i], _i),
-    "qlin_attn_decode_o_workspace_bytes": ([_i, _i, _l], _l),
-    "qlin_attn_decode_o_f16": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _p, _p, _l, _p, _i, _i, _l,
-                                _i, ctypes.c_float, _p, _p, _i, _i, _i, _p, _p, _p, _l, _p, _l,
-                                _p], _i),
 }
 
 
@@ -726,89 +721,6 @@ def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_
     rc = lib.qlin_attn_decode_rope(*args)
     _check(rc, "qlin_attn_decode_rope")
     return out
-
-
-_ATTN_O_WS = {}
-
-
-def _attn_o_workspace(lib, device, Hq, Hkv, L):
-    """Zero-filled workspace of qlin_attn_decode_o_f16, one per (device, stream), grown on demand
-    (the kernel leaves its counters zero; grow outside graph capture)."""
-    nbytes = lib.qlin_attn_decode_o_workspace_bytes(Hq, Hkv, L)
-    if nbytes < 0:
-        raise ValueError("attn_decode_o: unsupported shapes")
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    ws = _ATTN_O_WS.get(key)
-    if ws is None or ws.numel() * 4 < nbytes:
-        ws = torch.zeros(max(nbytes, 1 << 20) // 4, dtype=torch.int32, device=device)
-        _ATTN_O_WS[key] = ws
-    return ws
-
-
-def attn_decode_o_status(device):
-    """Nonzero when a qlin_attn_decode_o_f16 launch on this device's current stream gave up
-    waiting for its attention rows (bounded wait; the output of that launch is wrong)."""
-    ws = _ATTN_O_WS.get((device.index, torch.cuda.current_stream(device).cuda_stream))
-    return 0 if ws is None else int(ws[1152 // 4].item())
-
-
-def attn_decode_o_supported(n_heads, n_kv_heads, L, N, bits, group, flags):
-    return bool(load_library().qlin_attn_decode_o_supported(n_heads, n_kv_heads, L, N, bits, group,
-                                                           flags))
-
-
-def attn_decode_o(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads, head_dim,
-                  k_cache, v_cache, kv0, mask, scale_div, qweight, qsz, N, bits, group, flags,
-                  bias, residual):
-    """``qlin_attn_decode_o_f16``: ``attn_decode_rope`` (fp16 output) and the packed o_proj with
-    the residual epilogue, ``residual + o_proj(attn)``, in ONE launch for batch 1: q [1, 1, Hq*D],
-    k / v [1, 1, Hkv*D] fp16 row-strided views (before RoPE), caches as attn_decode_rope, o_proj
-    packed [N, Hq*D] (group multiple of 128), residual fp16 [1, 1, N] -> [1, 1, N] fp16."""
-    for t_ in (q, k, v):
-        if _rows(t_) is None:
-            raise ValueError("attn_decode_o takes row-strided [1, 1, H*D] q / k / v")
-    _on_gpu(q, k, v, cos_cache, sin_cache, position_ids, k_cache, v_cache, mask, qweight, qsz,
-            bias, residual)
-    L = kv0 + 1
-    if q.shape[0] != 1 or q.shape[1] != 1 or head_dim != ATTN_D:
-        raise ValueError("attn_decode_o: batch 1, one token, head_dim 128")
-    if not attn_decode_o_supported(n_heads, n_kv_heads, L, N, bits, group, flags):
-        raise ValueError("attn_decode_o: unsupported heads / o_proj shape")
-    for t_ in (q, k, v, k_cache, v_cache, residual):
-        if t_.dtype != torch.float16:
-            raise ValueError("attn_decode_o takes fp16 activations, caches and residual")
-    if not (k_cache.is_contiguous() and v_cache.is_contiguous()) or k_cache.shape != v_cache.shape \
-            or tuple(k_cache.shape[:2]) != (1, n_kv_heads) or k_cache.shape[3] != head_dim:
-        raise ValueError("attn_decode_o takes contiguous [1, Hkv, rows, D] caches of one shape")
-    if kv0 < 0 or L > k_cache.shape[2]:
-        raise ValueError(f"cache rows {k_cache.shape[2]} cannot take row {kv0}")
-    if cos_cache.dtype != torch.float32 or not cos_cache.is_contiguous() or \
-            sin_cache.dtype != torch.float32 or not sin_cache.is_contiguous():
-        raise ValueError("rope takes contiguous fp32 cos / sin caches")
-    if position_ids is None:
-        raise ValueError("attn_decode_o needs position_ids")
-    pos, _ = _pos_ids(position_ids, 1, 1)
-    m = None
-    if mask is not None:
-        if mask.dtype != torch.float16 or mask.shape[-1] != L or mask.shape[-2] != 1:
-            raise ValueError("attn_decode_o: mask fp16 [1, 1, 1, L]")
-        m = mask.reshape(1, L).contiguous()
-    if residual.numel() != N or not residual.is_contiguous():
-        raise ValueError("attn_decode_o: residual fp16 [1, 1, N] contiguous")
-    if bias is not None and (bias.dtype != torch.float16 or bias.numel() != N):
-        raise ValueError("attn_decode_o: bias fp16 [N]")
-    lib = load_library()
-    ws = _attn_o_workspace(lib, q.device, n_heads, n_kv_heads, L)
-    y = torch.empty(1, 1, N, dtype=torch.float16, device=q.device)
-    rows = k_cache.shape[2]
-    rc = lib.qlin_attn_decode_o_f16(
-        _ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(v), _rows(v), _ptr(cos_cache),
-        _ptr(sin_cache), cos_cache.shape[0], _ptr(pos), _ptr(k_cache), _ptr(v_cache),
-        rows * head_dim, _ptr(m), n_heads, n_kv_heads, L, head_dim, float(scale_div),
-        _ptr(qweight), _ptr(qsz), flags, bits, group, _ptr(bias), _ptr(residual), _ptr(y), N,
-        _ptr(ws), ws.numel() * 4, _stream(q))
-    _check(rc, "qlin_attn_decode_o_f16")
-    return y
 
 
 def attn_prefill_supported(q, k, mask=None):

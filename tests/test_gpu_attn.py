@@ -118,73 +118,6 @@ def test_attn_decode_rope_equals_two_launches(B, Hq, Hkv, kv0, rows, masked):
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("Hq,Hkv,kv0,N,bits,group,zf,masked,biased",
-                         [(32, 8, 512, 4096, 4, 128, 0, False, False),
-                          (32, 8, 4095, 4096, 4, 128, 0, True, False),
-                          (32, 8, 0, 4096, 3, 128, 0, False, True),
-                          (16, 4, 77, 2048, 2, 256, 0, True, False),
-                          (8, 8, 300, 1040, 8, 128, 1, False, True),
-                          (4, 1, 1500, 512, 4, 512, 0, True, False),
-                          (32, 16, 2049, 4096, 4, 128, 1, False, False)])
-def test_attn_decode_o_matches_two_launches(Hq, Hkv, kv0, N, bits, group, zf, masked, biased):
-    """qlin_attn_decode_o_f16 (decode attention + o_proj + residual in one launch): the cache rows
-    and the attention row bit-identical to qlin_attn_decode_rope; y = RN16(res + RN16(o_proj(attn)
-    + bias)) with o_proj against the dequantized weight in float64 (fp32 MFMA accumulation order:
-    within 1e-5 relative before the two fp16 roundings, i.e. at most 1 fp16 ulp apart)."""
-    from models.int_llama_layer import LlamaRotaryEmbedding437
-    D = 128
-    g = torch.Generator(device="cuda").manual_seed(kv0 + N)
-    qkv = (torch.randn(1, 1, (Hq + 2 * Hkv) * D, device="cuda", generator=g) * 2).half()
-    q, k, v = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
-    rot = LlamaRotaryEmbedding437(D, 8192, 500000.0, device="cuda").half()
-    cos, sin = rot.cos_cached.float().contiguous(), rot.sin_cached.float().contiguous()
-    pos = torch.full((1, 1), kv0, device="cuda", dtype=torch.int64)
-    rows = kv0 + 8
-    kc = torch.randn(1, Hkv, rows, D, device="cuda", generator=g).half()
-    vc = torch.randn(1, Hkv, rows, D, device="cuda", generator=g).half()
-    kc2, vc2 = kc.clone(), vc.clone()
-    mask = None
-    if masked:
-        mask = torch.zeros(1, 1, 1, kv0 + 1, device="cuda", dtype=torch.float16)
-        mask[..., : kv0 // 4] = torch.finfo(torch.float16).min
-    w = torch.randn(N, Hq * D, device="cuda", generator=g) * 0.02
-    o = qlin.quantize(w.half(), bits, group, zf, want_xdq=False, want_params=False, pack=True)
-    bias = (torch.randn(N, device="cuda", generator=g) * 0.1).half() if biased else None
-    res = torch.randn(1, 1, N, device="cuda", generator=g).half()
-    assert qlin.attn_decode_o_supported(Hq, Hkv, kv0 + 1, N, bits, group, o["flags"])
-    y = qlin.attn_decode_o(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, kv0, mask, math.sqrt(D),
-                           o["qweight"], o["qsz"], N, bits, group, o["flags"], bias, res)
-    att = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc2, vc2, kv0, mask,
-                                math.sqrt(D), out_dtype=torch.float16)
-    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
-    assert qlin.attn_decode_o_status(q.device) == 0
-    wdq = qlin.dequant(o["qweight"], o["qsz"], N, Hq * D, bits, group, o["flags"]).double()
-    x = att.reshape(1, Hq * D).double()
-    lin = x @ wdq.T + (0 if bias is None else bias.double())
-    yref = (res.double() + lin.half().double()).half().double().reshape(-1)
-    yd = y.double().reshape(-1)
-    eps = torch.finfo(torch.float16).eps
-    # the fp32 accumulation order may move RN16(o_proj) by one ulp and then y by one ulp
-    tol = eps * (lin.abs().reshape(-1) + yref.abs()) + 1.2e-7
-    assert ((yd - yref).abs() <= tol).all(), (yd - yref).abs().max().item()
-    assert (yd == yref).double().mean().item() >= 0.95
-    # repeated launches (counters left zero) and graph replays give the same bits
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        args = (q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, kv0, mask, math.sqrt(D), o["qweight"],
-                o["qsz"], N, bits, group, o["flags"], bias, res)
-        again = qlin.attn_decode_o(*args)
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr, stream=s):
-            out = qlin.attn_decode_o(*args)
-        for _ in range(3):
-            gr.replay()
-        assert qlin.attn_decode_o_status(q.device) == 0
-    torch.cuda.synchronize()
-    assert torch.equal(y, again) and torch.equal(y, out)
-
-
 def test_attn_decode_rejects_unsupported():
     q = torch.randn(1, 32, 1, 64, device="cuda")
     k = torch.randn(1, 8, 10, 64, device="cuda").half()

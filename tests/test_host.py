@@ -82,15 +82,6 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert gb(p, 256, p, 16, 0, p, 128, None, 0, p, 16, 70000, 1, 16, 128, 4, 128, None) == 1
     assert lib.qlin_attn_decode_splits(1, 8, 40) == 1 and lib.qlin_attn_decode_splits(1, 8, 0) == -1
     assert lib.qlin_attn_decode_splits(1, 8, 513) >= 2
-    # attention + o_proj in one launch: Hq % 4, Hq <= 32, whole-tile groups, no wide zeros
-    assert lib.qlin_attn_decode_o_supported(32, 8, 513, 4096, 4, 128, 0) == 1
-    assert lib.qlin_attn_decode_o_supported(64, 8, 513, 4096, 4, 128, 0) == 0
-    assert lib.qlin_attn_decode_o_supported(32, 8, 513, 4096, 4, 64, 0) == 0
-    assert lib.qlin_attn_decode_o_supported(32, 8, 4097, 4096, 4, 128, 0) == 0
-    assert lib.qlin_attn_decode_o_workspace_bytes(32, 8, 513) > 32 * 128 * 2
-    ao = lib.qlin_attn_decode_o_f16
-    assert ao(p, 4096, p, 1024, p, 1024, p, p, 8192, p, p, p, 1024 * 128, None, 32, 8, 513, 128,
-              11.3, p, p, 0, 4, 128, None, p, p, 4096, p, 0, None) == 1  # workspace too short
     assert lib.qlin_gemm_block_cols(0, 16, 4) == -1 and lib.qlin_gemm_block_cols(16, 16, 5) == -1
     assert lib.qlin_error_string(1) == b"invalid argument"
 
