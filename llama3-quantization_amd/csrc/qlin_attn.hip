@@ -91,6 +91,39 @@ __device__ __forceinline__ float part_load(const float* p) {
 #endif
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// wave-wide max / sum: DPP inside each 16-lane row (quad xor 1, quad xor 2, half-row mirror, row
+// mirror: after each step the partner group holds a uniform value, so mirrors act as xor 4 / 8),
+// then the 4 row results through readlane — a fixed order, no ds_bpermute round trips
+__device__ __forceinline__ float wave_max64(float v) {
+  v = fmaxf(v, dpp_f32<0xB1>(v));
+  v = fmaxf(v, dpp_f32<0x4E>(v));
+  v = fmaxf(v, dpp_f32<0x141>(v));
+  v = fmaxf(v, dpp_f32<0x140>(v));
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
+__device__ __forceinline__ float wave_sum64(float v) {
+  v += dpp_f32<0xB1>(v);
+  v += dpp_f32<0x4E>(v);
+  v += dpp_f32<0x141>(v);
+  v += dpp_f32<0x140>(v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 __device__ __forceinline__ float h2f(uint32_t w, int hi) {
   return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? (w >> 16) : (w & 0xFFFFu)));
 }
@@ -332,9 +365,13 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
       }
 #pragma unroll
       for (int g = 0; g < GRP; ++g) {
-        acc[g] += __shfl_xor(acc[g], 1);
-        acc[g] += __shfl_xor(acc[g], 2);
-        acc[g] += __shfl_xor(acc[g], 4);
+        // the xor-1 / xor-2 / xor-4 butterfly of the row's 8 lanes as DPP moves (ds_bpermute
+        // would be 3 dependent LDS round trips per head): after the two quad steps every lane of
+        // a quad holds the quad sum, so the half-row mirror (lane i <- 7 - i) reads the other
+        // quad's sum exactly as xor 4 would
+        acc[g] += dpp_f32<0xB1>(acc[g]);   // quad_perm [1, 0, 3, 2]
+        acc[g] += dpp_f32<0x4E>(acc[g]);   // quad_perm [2, 3, 0, 1]
+        acc[g] += dpp_f32<0x141>(acc[g]);  // row_half_mirror
       }
       if (t < n && sub < GRP) {
         // lane `sub` stores query head g = sub (select without dynamic register indexing)
@@ -354,14 +391,14 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   for (int g = wave; g < GRP; g += kWaves) {
     float m = -INFINITY;
     for (int t = lane; t < n; t += 64) m = fmaxf(m, sc[t][g]);
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    m = wave_max64(m);
     float s = 0.f;
     for (int t = lane; t < n; t += 64) {
       const float e = expf(sc[t][g] - m);
       sc[t][g] = e;
       s += e;
     }
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_sum64(s);
     if (lane == 0) {
       cm[g] = m;
       cl[g] = s;
@@ -369,30 +406,41 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   }
   __syncthreads();
 
-  // P V
+  // P V: branch-free (rows past the chunk: clamped reads, results selected away), the
+  // probabilities of RB rows read from LDS together (one LDS round trip per RB rows, not per row)
   {
+    constexpr int VR = kSub / kWaves;         // V rows per wave and pass
+    constexpr int RB = GRP <= 4 ? VR : VR / 2;  // rows per LDS batch (registers: RB x GRP)
     float a0[GRP], a1[GRP];
 #pragma unroll
     for (int g = 0; g < GRP; ++g) a0[g] = a1[g] = 0.f;
+    const uint32_t vn = has_new ? *reinterpret_cast<const uint32_t*>(&vnew[2 * lane]) : 0u;
     for (int tb = 0; tb < n; tb += kSub) {
-      uint32_t vc[kSub / kWaves];
+      uint32_t vc[VR];
 #pragma unroll
-      for (int u = 0; u < kSub / kWaves; ++u) {
-        vc[u] = vw[u];
-        if (has_new && t0 + tb + wave + kWaves * u == L - 1)
-          vc[u] = *reinterpret_cast<const uint32_t*>(&vnew[2 * lane]);
+      for (int u = 0; u < VR; ++u) {
+        const bool is_new = has_new && t0 + tb + wave + kWaves * u == L - 1;
+        vc[u] = is_new ? vn : vw[u];
       }
       if (tb + kSub < n) load_v(tb + kSub);
 #pragma unroll
-      for (int u = 0; u < kSub / kWaves; ++u) {
-        const int t = tb + wave + kWaves * u;
-        if (t < n) {
-          const float v0 = h2f(vc[u], 0), v1 = h2f(vc[u], 1);
+      for (int r0 = 0; r0 < VR; r0 += RB) {
+        float pr[RB][GRP];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int tc = min(tb + wave + kWaves * (r0 + r), n - 1);
+#pragma unroll
+          for (int g = 0; g < GRP; ++g) pr[r][g] = sc[tc][g];
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const bool ok = tb + wave + kWaves * (r0 + r) < n;
+          const float v0 = h2f(vc[r0 + r], 0), v1 = h2f(vc[r0 + r], 1);
 #pragma unroll
           for (int g = 0; g < GRP; ++g) {
-            const float p = sc[t][g];
-            a0[g] = fmaf(p, v0, a0[g]);
-            a1[g] = fmaf(p, v1, a1[g]);
+            const float f0 = fmaf(pr[r][g], v0, a0[g]), f1 = fmaf(pr[r][g], v1, a1[g]);
+            a0[g] = ok ? f0 : a0[g];
+            a1[g] = ok ? f1 : a1[g];
           }
         }
       }
@@ -468,14 +516,14 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   for (int g = wave; g < GRP; g += kWaves) {
     float M = -INFINITY;
     for (int s = lane; s < S; s += 64) M = fmaxf(M, mw[s][g]);
-    for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
+    M = wave_max64(M);
     float den = 0.f;
     for (int s = lane; s < S; s += 64) {
       const float w = expf(mw[s][g] - M);
       mw[s][g] = w;
       den += w * ml_l[s][g];
     }
-    for (int o = 32; o > 0; o >>= 1) den += __shfl_xor(den, o);
+    den = wave_sum64(den);
     if (lane == 0) cl[g] = den;
   }
   __syncthreads();

@@ -15,8 +15,10 @@ input), used by main.py:66-86 when a model does not fit one GPU.  Differences, b
   * decode (``generate``): greedy autoregressive decoding of several independent sequences
     (micro-batches) — each stage keeps the KV cache of its own layers for every micro-batch
     (the reference's per-layer ``past_key_value``, models/int_llama_layer.py:130-135, or the fused
-    layer's in-place cache buffers swapped in per micro-batch), the last stage picks each next
-    token and sends one [n_micro, B, 1] tensor back to the first stage per step.
+    layer's in-place cache buffers swapped in per micro-batch), the last stage picks each
+    micro-batch's next token and sends it back to the first stage at once, on a communicator of
+    its own, so stage 0 starts that micro-batch's next step while the later stages still run the
+    current one (no per-step drain).
   * transport: RCCL point-to-point with ``nccl``; with ``gloo`` device tensors are staged through
     host memory (gloo's send / recv take CPU tensors), e.g. several ranks sharing one GPU in tests.
 
@@ -87,20 +89,21 @@ class PipelineRunner:
         self.hidden_shape = tuple(hidden_shape)
         self.dtype = dtype
         self.device = torch.device(device)
+        self._tok_group = None
 
     def _host_staged(self):
         return dist.get_backend() == "gloo" and self.device.type != "cpu"
 
-    def _recv(self, shape=None, dtype=None, src=None):
+    def _recv(self, shape=None, dtype=None, src=None, group=None):
         shape = self.hidden_shape if shape is None else tuple(shape)
         dtype = self.dtype if dtype is None else dtype
         src = self.info.rank - 1 if src is None else src
         if self._host_staged():
             buf = torch.empty(shape, dtype=dtype)
-            dist.recv(buf, src=src)
+            dist.recv(buf, src=src, group=group)
             return buf.to(self.device)
         buf = torch.empty(shape, dtype=dtype, device=self.device)
-        dist.recv(buf, src=src)
+        dist.recv(buf, src=src, group=group)
         return buf
 
     def _bcast(self, t, src):
@@ -113,12 +116,12 @@ class PipelineRunner:
             dist.broadcast(t, src=src)
         return t
 
-    def _isend(self, t, dst):
+    def _isend(self, t, dst, group=None):
         """(request, the tensor kept alive until the request completes)"""
         t = t.contiguous()
         if self._host_staged():
             t = t.cpu()
-        return dist.isend(t, dst=dst), t
+        return dist.isend(t, dst=dst, group=group), t
 
     @torch.no_grad()
     def forward(self, micro_batches=None, n_micro=None):
@@ -195,33 +198,42 @@ class PipelineRunner:
         H = self.hidden_shape[-1]
         self._past, self._bufs = {}, {}
         out = torch.zeros(n_micro, B, n_new, dtype=torch.int64, device=self.device)
-        cur = None  # [n_micro, B, 1] next input tokens (first stage)
+        # next-token hand-back on a communicator of its own (first <-> last stage): each
+        # micro-batch's token leaves the last stage as soon as it is picked, and the first stage
+        # takes it just before that micro-batch's next step, so stage 0 starts micro-batch i of
+        # step s + 1 while later stages still run step s; a separate communicator keeps these
+        # transfers off the hidden-state stream's queue (RCCL runs one communicator's
+        # point-to-point operations in order)
+        if multi and getattr(self, "_tok_group", None) is None:
+            self._tok_group = dist.new_group([0, info.world - 1])  # collective: every rank
+        tok_group = self._tok_group if multi else None
+        cur = [None] * n_micro  # next input tokens [B, 1] per micro-batch (first stage)
+        tok_reqs, pending = [], []
         for step in range(n_new):
             T_in, pos0 = (T, 0) if step == 0 else (1, T + step - 1)
-            pending, nxt = [], []
             for i in range(n_micro):
                 if info.first:
-                    ids = prompts[i].to(self.device) if step == 0 else cur[i]
+                    if step == 0:
+                        ids = prompts[i].to(self.device)
+                    elif info.last:
+                        ids = cur[i]
+                    else:
+                        ids = self._recv((B, 1), torch.int64, src=info.world - 1, group=tok_group)
                     h = self.model.embed_tokens(ids)
                 else:
                     h = self._recv((B, T_in, H))
                 h = self._layers_step(h, i, pos0)
                 if info.last:
-                    nxt.append(self.model.head(h[:, -1:]).argmax(-1))  # [B, 1]
+                    tok = self.model.head(h[:, -1:]).argmax(-1)  # [B, 1]
+                    out[i, :, step] = tok[:, 0]
+                    if info.first:
+                        cur[i] = tok
+                    elif step + 1 < n_new:
+                        tok_reqs.append(self._isend(tok, 0, group=tok_group))
                 else:
                     pending.append(self._isend(h, info.rank + 1))
-            for req, _ in pending:
-                req.wait()
-            if info.last:
-                tok = torch.stack(nxt)  # [n_micro, B, 1]
-                out[:, :, step] = tok[:, :, 0]
-                if info.first:
-                    cur = tok
-                elif step + 1 < n_new:
-                    req, keep = self._isend(tok, 0)
-                    req.wait()
-            elif info.first and step + 1 < n_new:
-                cur = self._recv((n_micro, B, 1), torch.int64, src=info.world - 1)
+        for req, _ in pending + tok_reqs:  # no per-step drain: stages run ahead
+            req.wait()
         if multi:
             self._bcast(out, info.world - 1)
         return out

@@ -29,7 +29,8 @@ linear output) with only the summation order of F.linear changed:
 The order floor is the largest distance of a twin to the fake-quant logits (each twin's own
 distance is reported beside it).  The bar on every seed: each packed / fused
 path's max and p99 distance to the fake-quant logits <= 1.1 x the floor's, and its error against
-float64 <= 1.1 x the reference's.
+float64 <= 1.1 x the largest float64 error among the reference and its twins (the reference
+arithmetic's own spread: on seed 21 the F.linear-order twin alone is 1.12 x the reference).
 Numbers are written to $QLIN_PARITY_OUT (profiles/r4_decode_parity.json, r4_prefill_parity.json,
 r4_prefill32_parity.json)."""
 import json
@@ -199,8 +200,11 @@ def _judge(reps, ref_name="fake_quant", out_env=None):
         fq = rep[ref_name]
         fmax = max(rep[t]["logits_max_vs_fake_quant"] for t in TWINS)
         fp99 = max(rep[t]["logits_p99_vs_fake_quant"] for t in TWINS)
+        # the float64 bar, like the distance bar, is the reference arithmetic's own spread: the
+        # largest float64 error among the reference and its reorder twins
+        f64 = max([fq["logits_err_vs_fp64"]] + [rep[t]["logits_err_vs_fp64"] for t in TWINS])
         crit = {"max_vs_fake_quant": BAR * fmax, "p99_vs_fake_quant": BAR * fp99,
-                "err_vs_fp64": BAR * fq["logits_err_vs_fp64"],
+                "err_vs_fp64": BAR * f64, "order_floor_fp64": f64,
                 "order_floor_max": fmax, "order_floor_p99": fp99,
                 "order_floor_twins_max": {t: rep[t]["logits_max_vs_fake_quant"] for t in TWINS}}
         rep["criteria"] = crit

@@ -1,4 +1,4 @@
-"""Dev: per-wave timelines of the rows GEMV kernel (stamped build, GEMV_ROWS_STAMP): for each decode
+"""Dev: per-wave timelines of the rows / whole-row GEMV kernels (stamped build, GEMV_ROWS_STAMP): for each decode
 shape, a graph of dependent launches over a ring of distinct matrices; every launch records per
 wave s_memrealtime (100 MHz) at entry (0), prologue loads issued (1), x parked (2), first tile
 computed (3), last tile computed (4), exit (5).  Prints percentiles over waves, in us from the
@@ -69,6 +69,9 @@ for (name, N, K, ep, nrm) in SHAPES:
         v = S[i]
         valid = v[:, 0] > 0
         v = v[valid].double()
+        if v.shape[0] == 0:  # a kernel without stamps (the fast kernel)
+            print(f" launch {i}: no stamps", flush=True)
+            break
         t0 = v[:, 0].min()
         rel = (v - t0) / 100.0  # us
         q = lambda c, p: torch.quantile(rel[:, c], p).item()  # noqa: E731
@@ -81,5 +84,19 @@ for (name, N, K, ep, nrm) in SHAPES:
                   f"{q(2, .5):.2f}/{q(2, 1):.2f} first-tile p10/p50/p90 {q(3, .1):.2f}/{q(3, .5):.2f}/"
                   f"{q(3, .9):.2f} last-tile p10/p50/p90/max {q(4, .1):.2f}/{q(4, .5):.2f}/{q(4, .9):.2f}/"
                   f"{q(4, 1):.2f} exit max {q(5, 1):.2f}", flush=True)
+    if os.environ.get("STAMP_BREAKDOWN") and (S[ring - 1].view(nbmax, 16, 8)[:, :, 0] > 0).any():
+        v = S[ring - 1].view(nbmax, 16, 8)
+        blk = torch.arange(nbmax)[:, None].expand(nbmax, 16)
+        wv = torch.arange(16)[None, :].expand(nbmax, 16)
+        ok = v[:, :, 0] > 0
+        t0 = v[:, :, 0][ok].min()
+        last = (v[:, :, 4].double() - t0) / 100.0
+        for nm_, key in (("block % 8", blk % 8), ("wave", wv), ("block // 32", blk // 32)):
+            parts = []
+            for k_ in range(int(key[ok].max()) + 1):
+                sel = ok & (key == k_)
+                if sel.any():
+                    parts.append(f"{k_}:{last[sel].median().item():.2f}/{last[sel].max().item():.2f}")
+            print(f"   last-tile median/max by {nm_}: " + " ".join(parts), flush=True)
     del mats, g
     torch.cuda.empty_cache()
