@@ -623,17 +623,6 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
 // reference's rounding point after one block reduction of the sum of squares), and every A
 // fragment is a broadcast ds_read_b128 of it.  No barrier after the staging.
 // ---------------------------------------------------------------------------------------------
-#ifndef GEMV_WROW_PRIO  // dev knob: progress-based s_setprio in the whole-row kernel
-#define GEMV_WROW_PRIO 1
-#endif
-
-__device__ __forceinline__ void set_prio_remaining(int64_t rem) {
-  if (rem >= 4) __builtin_amdgcn_s_setprio(3);
-  else if (rem == 3) __builtin_amdgcn_s_setprio(2);
-  else if (rem == 2) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
-}
-
 constexpr int kWrowMaxWaves = 8;
 constexpr int kWrowXIter = 4;  // 16-B x chunks per thread (host: K <= 8 * 64 * waves * kWrowXIter)
 
@@ -795,13 +784,6 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
   };
   const int64_t rounds = (int64_t)nrow * (a.Kt / PF);
   for (int64_t rd = 0; rd + 1 < rounds; ++rd) {
-#if GEMV_WROW_PRIO
-    // progress-based wave priority: the CU serves older waves' requests first, so with equal
-    // priorities the younger waves of a block fall a round behind and finish ~3 us after the
-    // others (stamped, gate/up: waves 0-3 at 10.8 us, waves 4-6 at 14.1 us); a wave with more
-    // rounds left issues first
-    set_prio_remaining(rounds - rd);
-#endif
     lkt += PF;
     if (lkt == a.Kt) {  // wave-uniform: the load cursor moves to the wave's next row
       lkt = 0;
@@ -829,192 +811,6 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
   for (int u = 0; u < PF; ++u) compute(u);
   ROWS_STAMP(4);
   store();
-  ROWS_STAMP(5);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Decode path for wide matrices, K-quarter form (gate/up: 1,792 tile rows, 7 per CU).
-//
-// Stamped, the whole-row kernel above is SIMD-bound, not HBM-bound, on its wide launch: with 7
-// waves per CU, SIMDs 0-2 run two row-waves and SIMD 3 one, and the dequant VALU of two whole
-// rows (2 x 32 tiles x 52 VALU) takes longer than the stream; waves 0-3 finish at 10.8-12.3 us,
-// waves 4-6 at 14.1 (tools/dev/rows_stamps.py, STAMP_BREAKDOWN).  Here a block of 8 waves (2 per
-// SIMD) owns R tile rows (b, b + nb, ...) and wave w streams K quarter w & 3 (TQ = Kt / 4 tiles,
-// the prefetch round) of rows w >> 2, (w >> 2) + 2, ... — every SIMD gets the same share of each
-// row, so the tiles (and their VALU) split evenly over the SIMDs whatever R is.  Each quarter is
-// one MFMA chain in k order, parked in LDS; after one barrier the four quarters of every output
-// are added in a fixed order ((q0 + q1) + (q2 + q3)) and the epilogue runs (bias, the fp16
-// rounding, residual or SiLU * up over the interleaved halves).  x is staged once per block in
-// LDS (RMSNorm applied at the reference's rounding point) as in the whole-row kernel.
-// ---------------------------------------------------------------------------------------------
-constexpr int kQuadWaves = 8;
-constexpr int kQuadMaxRows = 16;  // tile rows per block
-
-template <int BITS, int GPT, int ZM, int TQ, bool NRM>
-__global__ __launch_bounds__(64 * kQuadWaves) void gemv_quad_kernel(const WrowArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xs4[];  // x (normed), fp16 [K]
-  __shared__ float nss[kQuadWaves];
-  __shared__ float part[4][kQuadMaxRows][kTileN];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63, n_in = lane & 15, lq = lane >> 4;
-  constexpr int nthr = 64 * kQuadWaves;
-  const int qk = wave & 3, hph = wave >> 2;  // K quarter, row phase
-  const int nb = a.nwaves, b = blockIdx.x;
-  const int R = b < a.Nt ? (a.Nt - 1 - b) / nb + 1 : 0;  // tile rows of this block
-  const int nu = R > hph ? (R - 1 - hph) / 2 + 1 : 0;    // units of this wave (wave-uniform)
-  ROWS_STAMP(0);
-  auto group_of_tile = [&](int kt) {
-    return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
-  };
-
-  // x chunks of this thread first (clamped: repeats are never stored), and the epilogue
-  // operands of the thread's output (t < R * 16: local row t / 16, column t % 16), both
-  // unconditional (absent operands point at y)
-  const int nch = a.K >> 3;
-  uint4 xc[kWrowXIter];
-  float4 nc[NRM ? 2 * kWrowXIter : 1];
-#pragma unroll
-  for (int i = 0; i < kWrowXIter; ++i) {
-    const int c = min(tid + i * nthr, nch - 1);
-    xc[i] = reinterpret_cast<const uint4*>(a.x)[c];
-    if constexpr (NRM) {
-      nc[2 * i] = reinterpret_cast<const float4*>(a.nw)[2 * c];
-      nc[2 * i + 1] = reinterpret_cast<const float4*>(a.nw)[2 * c + 1];
-    }
-  }
-  const int ejr = min(tid >> 4, kQuadMaxRows - 1), en = tid & 15;
-  const int64_t erow = (int64_t)(b + (int64_t)nb * ejr) * kTileN;  // first output row of the tile
-  const int NO = a.ep == kEpSiluMul ? 8 : kTileN;
-  const int64_t nb_ = a.has_bias ? (int64_t)a.N : a.nres;  // readable bias elements
-  const _Float16 ob = a.bias[min(erow + en, nb_ - 1)];
-  const _Float16 ores = a.res[min(erow + min(en, NO - 1), a.nres - 1)];
-  // every wave's x requests enter the CU's memory queue ahead of any tile request
-  asm volatile("s_barrier" ::: "memory");
-
-  // unit i of this wave: tile row b + nb * (hph + 2 i), k-tiles qk * TQ .. qk * TQ + TQ - 1
-  WTile<BITS, GPT> wt[TQ];
-  const int64_t wrow = (int64_t)a.Kt * (64 * BITS), srow = (int64_t)a.G * kTileN;
-  const uint32_t* lqw = nullptr;
-  const uint32_t* lsz = nullptr;
-  auto set_unit = [&](int i) {
-    const int64_t r = b + (int64_t)nb * (hph + 2 * i);
-    lqw = a.qw + r * wrow + (int64_t)qk * TQ * (64 * BITS) + lane * BITS;
-    lsz = a.qsz + r * srow + n_in;
-  };
-  auto load = [&](int j) {
-    wt[j].pc = load_piece_nt<BITS>(lqw + j * (64 * BITS));
-    const int g0 = group_of_tile(qk * TQ + j);
-#pragma unroll
-    for (int s = 0; s < GPT; ++s) wt[j].sz[s] = lsz[(g0 + s) * kTileN];
-  };
-  if (nu > 0) {  // wave-uniform
-    set_unit(0);
-#pragma unroll
-    for (int j = 0; j < TQ; ++j) load(j);
-  }
-  ROWS_STAMP(1);
-
-  // stage x (normed) in LDS: one block reduction for the statistics, one barrier
-  if constexpr (NRM) {
-#pragma clang fp contract(off)
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < kWrowXIter; ++i) {
-      const h8 v = __builtin_bit_cast(h8, xc[i]);
-      float s8 = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s8 = s8 + (float)v[j] * (float)v[j];
-      ss = ss + (tid + i * nthr < nch ? s8 : 0.f);
-    }
-    ss = wave_sum(ss);
-    if (lane == 0) nss[wave] = ss;
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    float tot = 0.f;
-    for (int w = 0; w < kQuadWaves; ++w) tot += nss[w];
-    const float rn = rsqrtf(tot / (float)a.K + a.eps);
-#pragma unroll
-    for (int i = 0; i < kWrowXIter; ++i) {
-      const h8 v = __builtin_bit_cast(h8, xc[i]);
-      const float w8[8] = {nc[2 * i].x, nc[2 * i].y, nc[2 * i].z, nc[2 * i].w,
-                           nc[2 * i + 1].x, nc[2 * i + 1].y, nc[2 * i + 1].z, nc[2 * i + 1].w};
-      h8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (_Float16)(w8[j] * ((float)v[j] * rn));
-      xc[i] = __builtin_bit_cast(uint4, o);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < kWrowXIter; ++i)
-    if (tid + i * nthr < nch) xs4[tid + i * nthr] = xc[i];
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  ROWS_STAMP(2);
-
-  const Magics mg = make_magics<BITS>();
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int j) {
-    const int kt = qk * TQ + j;
-    h8 xa[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, xs4[kt * 16 + 4 * s + lq]);
-    auto step = [&](auto S_) {
-      constexpr int S = decltype(S_)::value;
-      uint32_t v[4];
-      const GroupQ gq = make_group_w<BITS, ZM>(wt[j].sz[S * GPT / 4]);
-      dequant_step<BITS, ZM, S>(wt[j].pc, mg, gq, v);
-      const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
-    };
-    step(std::integral_constant<int, 0>{});
-    step(std::integral_constant<int, 1>{});
-    step(std::integral_constant<int, 2>{});
-    step(std::integral_constant<int, 3>{});
-  };
-  auto park = [&](int i) {  // C row 0 = acc[0] of lanes 0..15 (column n = lane)
-    if (lane < kTileN) part[qk][hph + 2 * i][lane] = acc[0];
-    acc = f4{0.f, 0.f, 0.f, 0.f};
-  };
-  if (nu > 0) {
-    for (int i = 0; i + 1 < nu; ++i) {
-      set_unit(i + 1);
-#pragma unroll
-      for (int j = 0; j < TQ; ++j) {
-        compute(j);
-#ifdef GEMV_ROWS_STAMP
-        if (i == 0 && j == 0) ROWS_STAMP(3);
-#endif
-        load(j);
-      }
-      park(i);
-    }
-#pragma unroll
-    for (int j = 0; j < TQ; ++j) compute(j);
-    ROWS_STAMP(4);
-    park(nu - 1);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-
-  // the four quarters of every output, in a fixed order, then the epilogue
-  if (tid < R * kTileN) {
-    const int jr = tid >> 4;
-    auto total = [&](int n) {
-      return (part[0][jr][n] + part[1][jr][n]) + (part[2][jr][n] + part[3][jr][n]);
-    };
-    float t = total(en);
-    if (a.has_bias) t += (float)ob;
-    t = (float)(_Float16)t;  // F.linear's fp16 output
-    if (a.ep == kEpSiluMul) {
-      if (en < 8) {
-        float up = total(en + 8);
-        if (a.has_bias) up += (float)a.bias[min(erow + en + 8, nb_ - 1)];
-        up = (float)(_Float16)up;
-        if (erow + en + 8 < a.N) a.y[erow / 2 + en] = (_Float16)(silu_rn16(t) * up);
-      }
-    } else if (erow + en < a.N) {
-      if (a.ep == kEpResidual) t += (float)ores;
-      a.y[erow + en] = (_Float16)t;
-    }
-  }
   ROWS_STAMP(5);
 }
 
@@ -1383,64 +1179,6 @@ int launch_wrow_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
 #undef QLIN_WG
 }
 
-// ---- M == 1, wide matrices: the K-quarter kernel ------------------------------------------------
-#ifndef GEMV_QUAD  // dev knob: 0 = wide launches stay on the whole-row kernel
-#define GEMV_QUAD 1
-#endif
-// blocks = CUs (R = ceil(Nt / CUs) <= 16 rows each), TQ = Kt / 4 in {4, 8} tiles per quarter
-static inline bool quad_geometry(int64_t Nt, int Kt, int K, int& nb, int& tq) {
-  if (!GEMV_QUAD) return false;
-  const int64_t cus = device_cu_count();
-  if (Nt < GEMV_WROW_MIN_ROWS_CU * cus || Kt % 4 || !(Kt / 4 == 4 || Kt / 4 == 8)) return false;
-  nb = (int)cus;
-  tq = Kt / 4;
-  return (Nt + cus - 1) / cus <= kQuadMaxRows && (int64_t)kQuadWaves * 64 * kWrowXIter * 8 >= K;
-}
-
-template <int BITS, int ZM>
-int launch_quad_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
-                  uint16_t* y, int N, int K, int group, hipStream_t st, int ep,
-                  const uint16_t* res, const float* nw, float eps, int nb, int tq) {
-  WrowArgs a;
-#ifdef GEMV_ROWS_STAMP
-  a.stamps = g_rows_stamps;
-#endif
-  a.qw = qw;
-  a.qsz = qsz;
-  a.x = (const _Float16*)x;
-  a.has_bias = bias != nullptr;
-  a.bias = (const _Float16*)(bias ? bias : y);
-  a.res = (const _Float16*)(ep == kEpResidual ? res : y);
-  a.nres = ep == kEpSiluMul ? N / 2 : N;
-  a.y = (_Float16*)y;
-  a.nw = nw;
-  a.eps = eps;
-  a.ep = ep;
-  a.N = N;
-  a.K = K;
-  a.Kt = K / kTileK;
-  a.G = K / group;
-  a.Nt = (N + kTileN - 1) / kTileN;
-  a.nwaves = nb;  // the grid's blocks
-  a.cmagic = tile_group_magic(group);
-  const size_t lds = (size_t)K * 2;
-#define QLIN_QD(GPT, TQ, NRM)                                                                   \
-  hipLaunchKernelGGL((gemv_quad_kernel<BITS, GPT, ZM, TQ, NRM>), dim3((unsigned)nb),           \
-                     dim3(64 * kQuadWaves), lds, st, a)
-#define QLIN_QT(GPT, NRM)          \
-  if (tq == 8) QLIN_QD(GPT, 8, NRM); \
-  else QLIN_QD(GPT, 4, NRM)
-#define QLIN_QG(GPT)               \
-  if (nw) QLIN_QT(GPT, true);      \
-  else QLIN_QT(GPT, false)
-  if (group % kTileK == 0) QLIN_QG(1);
-  else QLIN_QG(2);  // group 64 (m1_route keeps 32 off this kernel)
-#undef QLIN_QG
-#undef QLIN_QT
-#undef QLIN_QD
-  return (int)hipGetLastError();
-}
-
 // ---- M == 1: the rows kernel ------------------------------------------------------------------
 struct RowsGeo {
   int W, TPW, nb, pf;
@@ -1613,15 +1351,13 @@ int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
 // (tools/dev/rows_sweep.py: gate/up 28,672 x 4,096 whole-row 15.3 us vs fast 15.4 / rows 15.6;
 // down 4,096 x 14,336 rows 8.25 us vs gemv_kernel 8.7; 4096^2 and q/k/v fast 3.7 / 5.7 us vs rows
 // 3.8-4.2 / 6.1)
-enum { kM1None = 0, kM1Wrow, kM1Fast, kM1Rows, kM1Quad };
+enum { kM1None = 0, kM1Wrow, kM1Fast, kM1Rows };
 static inline int m1_route(int64_t N, int K, int group, const void* x, const float* nw, WrowGeo& wg,
                            int& W, int& lw, int& tpw, RowsGeo& rg) {
   if (!group_fast(K, group)) return kM1None;
   const int64_t Nt = (N + kTileN - 1) / kTileN;
   const int Kt = K / kTileK;
   const bool aligned = ((uintptr_t)x & 15) == 0 && ((uintptr_t)nw & 15) == 0 && K % 8 == 0;
-  // (32-wide groups stay on the whole-row kernel: four (scale, zero) words per tile spill here)
-  if (aligned && group != 32 && quad_geometry(Nt, Kt, K, wg.nb, wg.pf)) return kM1Quad;
   if (aligned && wrow_geometry(Nt, Kt, K, wg)) return kM1Wrow;
   if (Nt <= (1 << 26) && fast_geometry((int)Nt, Kt, W, lw, tpw)) return kM1Fast;
   if (rows_geometry(Nt, Kt, rg)) return kM1Rows;
@@ -1636,9 +1372,6 @@ int launch_m1(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const 
   RowsGeo rg;
   int W = 0, lw = 0, tpw = 0;
   switch (m1_route(N, K, group, x, nw, wg, W, lw, tpw, rg)) {
-    case kM1Quad:
-      return launch_quad_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, ep, res, nw, eps,
-                                     wg.nb, wg.pf);
     case kM1Wrow:
       return launch_wrow_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, ep, res, nw, eps, wg);
     case kM1Fast:
