@@ -674,11 +674,6 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
     }
   }
 
-  // every wave's x requests enter the CU's memory queue before any wave's tile requests: the
-  // x staging barrier below waits for the slowest wave's x, which otherwise queues behind the
-  // other waves' tiles (stamped: x staged at 3.8 us instead of ~1.5, tools/dev/rows_stamps.py)
-  asm volatile("s_barrier" ::: "memory");
-
   // the first PF tiles of the wave's first row (rows of PF-tile rounds: Kt % PF == 0)
   WTile<BITS, GPT> wt[PF];
   const int64_t wrow = (int64_t)a.Kt * (64 * BITS), srow = (int64_t)a.G * kTileN;
