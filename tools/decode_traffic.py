@@ -11,7 +11,8 @@ import json
 import os
 import sys
 
-LAYER_KERNELS = ("gemv_fast_kernel", "gemv_kernel", "attn_decode_kernel")
+LAYER_KERNELS = ("gemv_fast_kernel", "gemv_kernel", "gemv_wrow_kernel", "gemv_rows_kernel",
+                 "attn_decode_kernel")
 
 
 def main():
