@@ -284,6 +284,23 @@ int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_
                           float scale_div, float* partials, int32_t* counters, void* stream);
 
 /*
+ * qlin_attn_decode_rope for a graph-replayed decode step (mask NULL, position_ids required): the
+ * cache length is read on the device from len[0] (1 <= len[0] <= L_cap), so one captured launch
+ * serves every step; L_cap (the cache capacity used at capture) sizes the grid and the partials
+ * (qlin_attn_decode_partials_bytes(B, Hq, Hkv, L_cap)); blocks past the step's length exit.  The
+ * split of the rows depends on L_cap, not on len[0]: same arithmetic as qlin_attn_decode_rope at
+ * L = L_cap for the rows present (results agree with it to fp32 summation order).
+ */
+int qlin_attn_decode_rope_len(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+                              int64_t k_row_stride, const uint16_t* v, int64_t v_row_stride,
+                              const float* cos_cache, const float* sin_cache, int64_t cache_rows,
+                              const int64_t* position_ids, int64_t pos_batch_stride,
+                              uint16_t* k_cache, uint16_t* v_cache, int64_t kv_head_stride,
+                              void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L_cap,
+                              int D, float scale_div, float* partials, int32_t* counters,
+                              const int32_t* len, void* stream);
+
+/*
  * Fused prefill attention (many query tokens per sequence): the same attention core as
  * qlin_attn_decode — repeat_kv, fp32 QK^T, / sqrt(head_dim) (as torch: x the fp32 reciprocal),
  * + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV (models/int_llama_layer.py:137-165 of

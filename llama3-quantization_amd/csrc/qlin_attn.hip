@@ -165,14 +165,16 @@ struct AttnArgs {
   float* part_o;
   float* part_ml;
   RopeIn ri;
+  const int* len;  // NULL, or the device-resident cache length (L is then the capacity: the
+                   // grid and the partials are sized for it; blocks past the length exit)
 #ifdef ATTN_STAMP
   uint64_t* stamps;
 #endif
 };
 
 // dev build only (tools/dev/attn_stamps.py): s_memrealtime (100 MHz) per block [block][8] at
-// 0 start, 1 q ready, 2 scores (K landed), 3 P V (V landed), 4 partials counted, 5 merge inputs
-// loaded, 6 output stored
+// 0 start, 1 q ready, 2 scores (K landed), 7 softmax statistics, 3 P V (V landed), 4 partials
+// counted, 5 merge inputs loaded, 6 output stored
 #ifdef ATTN_STAMP
 inline uint64_t* g_attn_stamps = nullptr;
 #define AT_STAMP(P, k)                                                                          \
@@ -190,7 +192,12 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   const _Float16* __restrict__ v = A.v;
   const _Float16* __restrict__ mask = A.mask;
   void* __restrict__ out = A.out;
-  const int out_f16 = A.out_f16, Hq = A.Hq, Hkv = A.Hkv, L = A.L, chunk = A.chunk, S = A.S;
+  const int out_f16 = A.out_f16, Hq = A.Hq, Hkv = A.Hkv, chunk = A.chunk;
+  const int Sl = A.S;  // partials layout: split slots per (b, kv head)
+  // device-resident length (graph-replayed decode steps): L and the split count of this step
+  const int L = A.len ? min(max(__builtin_amdgcn_readfirstlane(*A.len), 1), A.L) : A.L;
+  const int S = A.len ? (L + chunk - 1) / chunk : Sl;
+  if (split >= S) return;  // block-uniform: past this step's length
   const int64_t kv_hs = A.kv_hs;
   const float scale_div = A.scale_div;
   int* __restrict__ counters = A.counters;
@@ -405,6 +412,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     }
   }
   __syncthreads();
+  AT_STAMP(A, 7);
 
   // P V: branch-free (rows past the chunk: clamped reads, results selected away), the
   // probabilities of RB rows read from LDS together (one LDS round trip per RB rows, not per row)
@@ -471,11 +479,11 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   }
 
   // write this chunk's partials, then count in; the last block of (b, kv head) merges
-  float* pob = part_o + ((int64_t)bh * S + split) * GRP * kD;
+  float* pob = part_o + ((int64_t)bh * Sl + split) * GRP * kD;
   for (int o = tid; o < GRP * kD; o += kThreads)
     part_store(pob + o, po[0][o] + po[1][o] + po[2][o] + po[3][o]);
   if (tid < 2 * GRP) {
-    float* ml = part_ml + ((int64_t)bh * S + split) * GRP * 2;
+    float* ml = part_ml + ((int64_t)bh * Sl + split) * GRP * 2;
     part_store(ml + tid, (tid & 1) ? cl[tid >> 1] : cm[tid >> 1]);
   }
 #if ATTN_FENCE_MODE == 0
@@ -498,7 +506,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   // the chunk statistics — one memory round trip instead of two at decode lengths (S <= 16)
   constexpr int J = GRP * kD / 64;
   constexpr int kPre = GRP <= 4 ? 4 : 2;
-  const float* pb = part_o + (int64_t)bh * S * GRP * kD + lane;
+  const float* pb = part_o + (int64_t)bh * Sl * GRP * kD + lane;
   float xpre[kPre][J];
 #pragma unroll
   for (int i = 0; i < kPre; ++i) {
@@ -507,7 +515,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     for (int j = 0; j < J; ++j) xpre[i][j] = part_load(pb + (int64_t)s * GRP * kD + 64 * j);
   }
   // chunk statistics -> weights exp(m_s - M) and denominators sum_s w_s l_s
-  const float* mlb = part_ml + (int64_t)bh * S * GRP * 2;
+  const float* mlb = part_ml + (int64_t)bh * Sl * GRP * 2;
   for (int i = tid; i < S * GRP; i += kThreads) {
     mw[i / GRP][i % GRP] = part_load(mlb + 2 * i);
     ml_l[i / GRP][i % GRP] = part_load(mlb + 2 * i + 1);
@@ -578,12 +586,12 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(const AttnArgs A)
 int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const uint16_t* mask,
                   void* out, int out_dtype, int64_t B, int Hq, int Hkv, int64_t L, int64_t kv_hs,
                   float scale_div, float* part_o, float* part_ml, int32_t* counters,
-                  const Split& sp, hipStream_t st, const RopeIn& ri) {
+                  const Split& sp, hipStream_t st, const RopeIn& ri, const int* len = nullptr) {
   const dim3 grid((unsigned)(B * Hkv), (unsigned)sp.S);
   const int grp = Hq / Hkv;
   AttnArgs A{q, (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,
                    out_dtype == QLIN_F16, Hq, Hkv, (int)L, kv_hs, sp.chunk, sp.S, scale_div,
-                   (int*)counters, part_o, part_ml, ri};
+                   (int*)counters, part_o, part_ml, ri, len};
 #ifdef ATTN_STAMP
   A.stamps = g_attn_stamps;
 #endif
@@ -655,7 +663,8 @@ static int attn_decode_rope_impl(const uint16_t* q, int64_t q_row_stride, const 
                                      uint16_t* k_cache, uint16_t* v_cache, int64_t kv_head_stride,
                                      const uint16_t* mask, void* out, int out_dtype, int64_t B,
                                      int Hq, int Hkv, int64_t L, int D, float scale_div,
-                                     float* partials, int32_t* counters, void* stream) {
+                                     float* partials, int32_t* counters, void* stream,
+                                     const int32_t* len = nullptr) {
   // position_ids NULL: cos_cache / sin_cache are the rows of the step's position (B == 1)
   if (!position_ids && B > 1) return QLIN_EINVAL;
   if (!q || !k || !v || !cos_cache || !sin_cache || !k_cache || !v_cache ||
@@ -682,7 +691,7 @@ static int attn_decode_rope_impl(const uint16_t* q, int64_t q_row_stride, const 
                   position_ids, pos_batch_stride, (_Float16*)k_cache, (_Float16*)v_cache};
   return launch_decode(nullptr, k_cache, v_cache, mask, out, out_dtype, B, Hq, Hkv, L,
                        kv_head_stride, scale_div, part_o, part_ml, counters, sp,
-                       (hipStream_t)stream, ri);
+                       (hipStream_t)stream, ri, len);
 }
 
 extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
@@ -698,6 +707,23 @@ extern "C" int qlin_attn_decode_rope(const uint16_t* q, int64_t q_row_stride, co
                                sin_cache, cache_rows, position_ids, pos_batch_stride, k_cache,
                                v_cache, kv_head_stride, mask, out, out_dtype, B, Hq, Hkv, L, D,
                                scale_div, partials, counters, stream);
+}
+
+extern "C" int qlin_attn_decode_rope_len(const uint16_t* q, int64_t q_row_stride, const uint16_t* k,
+                                         int64_t k_row_stride, const uint16_t* v,
+                                         int64_t v_row_stride, const float* cos_cache,
+                                         const float* sin_cache, int64_t cache_rows,
+                                         const int64_t* position_ids, int64_t pos_batch_stride,
+                                         uint16_t* k_cache, uint16_t* v_cache,
+                                         int64_t kv_head_stride, void* out, int out_dtype,
+                                         int64_t B, int Hq, int Hkv, int64_t L_cap, int D,
+                                         float scale_div, float* partials, int32_t* counters,
+                                         const int32_t* len, void* stream) {
+  if (!len || !position_ids) return QLIN_EINVAL;
+  return attn_decode_rope_impl(q, q_row_stride, k, k_row_stride, v, v_row_stride, cos_cache,
+                               sin_cache, cache_rows, position_ids, pos_batch_stride, k_cache,
+                               v_cache, kv_head_stride, nullptr, out, out_dtype, B, Hq, Hkv,
+                               L_cap, D, scale_div, partials, counters, stream, len);
 }
 
 extern "C" int qlin_attn_decode_splits(int64_t B, int Hkv, int64_t L) {

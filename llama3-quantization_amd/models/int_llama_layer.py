@@ -297,6 +297,29 @@ class QuantLlamaAttention(nn.Module):
             self._rope32_key = key
         return self._rope32
 
+    # graph-replayed decode steps (models/pipeline.py generate(graphs=True)): an int32 device
+    # tensor holding the step's cache length; the step then reads nothing on the host (no past /
+    # mask / length checks), appends to and attends over the kv_cache buffers in self._kv
+    _dyn_len = None
+
+    def _decode_step_len(self, hidden_states, position_ids, residual, prenorm):
+        """One token through the fused packed attention with the cache length on the device
+        (qlin_attn_decode_rope_len over self._kv's capacity): a launch sequence that stays valid
+        for every step, so it can be captured once and replayed."""
+        bsz = hidden_states.shape[0]
+        act_dtype = hidden_states.dtype
+        if not (self.kv_cache and self._kv is not None and act_dtype == torch.float16
+                and position_ids is not None):
+            raise ValueError("device-length decode needs kv_cache buffers, fp16 and position_ids")
+        q, k, v = self._project(hidden_states, prenorm)
+        buf = self._kv
+        cos_c, sin_c = self._rope_cache(buf[0], buf[0].shape[2])
+        attn = qlin.attn_decode_rope_len(q, k, v, cos_c, sin_c, position_ids, self.num_heads,
+                                         self.num_key_value_heads, self.head_dim, buf[0], buf[1],
+                                         self._dyn_len, out_dtype=torch.float16)
+        attn = attn.transpose(1, 2).reshape(bsz, 1, self.hidden_size)
+        return self._out(attn, residual), None, None
+
     def _out(self, attn_output, residual):
         if residual is None:
             return self.o_proj(attn_output)
@@ -324,6 +347,8 @@ class QuantLlamaAttention(nn.Module):
         token row)."""
         bsz, q_len, _ = hidden_states.size()
         act_dtype = hidden_states.dtype
+        if self._dyn_len is not None and q_len == 1:
+            return self._decode_step_len(hidden_states, position_ids, residual, prenorm)
         kv_seq_len = q_len
         if past_key_value is not None:
             kv_seq_len += past_key_value[0].shape[-2]

@@ -175,13 +175,74 @@ class PipelineRunner:
                 bufs[j] = at._kv
         return h
 
+    def _layers_step_len(self, h, mb, pos, length):
+        """This stage's layers over one token per sequence with the cache length on the device
+        (each layer's attention in its device-length mode over micro-batch ``mb``'s buffers):
+        the launch sequence of every decode step, captured once per micro-batch."""
+        n = len(self.model.layers)
+        bufs = self._bufs[mb]
+        for j, layer in enumerate(self.model.layers):
+            at = layer.self_attn
+            at._kv = bufs[j]
+            at._dyn_len = length
+            try:
+                h = layer(h, attention_mask=None, position_ids=pos, past_key_value=None,
+                          use_cache=False)[0]
+            finally:
+                at._dyn_len = None
+        return h
+
+    def _graph_step(self, h, mb, pos0, cap_rows, replay):
+        """Decode step of micro-batch ``mb`` at position pos0 through the device-length layers:
+        replayed from its HIP graph (captured at its first step) when ``replay``, else eager —
+        the same launches either way, so both give the same bits."""
+        st = self._gstate.get(mb)
+        if st is None:
+            B, T, H = h.shape
+            # every layer's cache buffers must hold all the steps: grow them once, here
+            for j, layer in enumerate(self.model.layers):
+                at = layer.self_attn
+                kb, vb = self._bufs[mb][j]
+                if kb.shape[2] < cap_rows:
+                    at.adopt_kv_cache((kb[:, :, :pos0], vb[:, :, :pos0]), rows=cap_rows)
+                    self._bufs[mb][j] = at._kv
+            st = {"h": torch.empty_like(h), "pos": torch.empty(B, 1, dtype=torch.int64,
+                                                                 device=h.device),
+                  "len": torch.empty(1, dtype=torch.int32, device=h.device), "graph": None}
+            self._gstate[mb] = st
+        st["h"].copy_(h)
+        st["pos"].fill_(pos0)
+        st["len"].fill_(pos0 + 1)
+        if not replay:
+            return self._layers_step_len(st["h"], mb, st["pos"], st["len"])
+        if st["graph"] is None:
+            # one eager pass first (workspaces, rotary tables), then the capture; both rewrite
+            # the same cache row pos0 with the same values before the replay below
+            s_ = torch.cuda.Stream(h.device)
+            s_.wait_stream(torch.cuda.current_stream(h.device))
+            with torch.cuda.stream(s_):
+                self._layers_step_len(st["h"], mb, st["pos"], st["len"])
+            torch.cuda.current_stream(h.device).wait_stream(s_)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st["out"] = self._layers_step_len(st["h"], mb, st["pos"], st["len"])
+            st["graph"] = g
+        st["graph"].replay()
+        return st["out"].clone()
+
     @torch.no_grad()
-    def generate(self, prompts=None, n_new=8):
+    def generate(self, prompts=None, n_new=8, graphs=False, device_len=None):
         """Greedy decoding of independent sequences through the pipeline.  ``prompts``: list of
         int64 token tensors [B, T] (one micro-batch each, same shape), needed on the first stage
         only.  Step 0 runs the prompts (prefill) and picks the first new token; each later step
         runs one token per sequence over the stages' KV caches.  Returns int64 [n_micro, B, n_new]
-        on every rank."""
+        on every rank.
+
+        ``graphs`` (GPU, fused packed layers in kv_cache mode): decode steps run each stage's
+        layers in their device-length form (the cache length read on the device), captured into
+        one HIP graph per micro-batch at its first decode step and replayed after;
+        ``device_len=True`` runs that form eagerly (same bits as the graphs)."""
+        device_len = graphs if device_len is None else device_len
         info = self.info
         multi = info.world > 1
         meta = torch.zeros(3, dtype=torch.int64)
@@ -196,7 +257,7 @@ class PipelineRunner:
             meta = self._bcast(meta.to(self.device), 0).cpu()
         n_micro, B, T = (int(v) for v in meta.tolist())
         H = self.hidden_shape[-1]
-        self._past, self._bufs = {}, {}
+        self._past, self._bufs, self._gstate = {}, {}, {}
         out = torch.zeros(n_micro, B, n_new, dtype=torch.int64, device=self.device)
         # next-token hand-back on a communicator of its own (first <-> last stage): each
         # micro-batch's token leaves the last stage as soon as it is picked, and the first stage
@@ -222,7 +283,10 @@ class PipelineRunner:
                     h = self.model.embed_tokens(ids)
                 else:
                     h = self._recv((B, T_in, H))
-                h = self._layers_step(h, i, pos0)
+                if step > 0 and device_len:
+                    h = self._graph_step(h, i, pos0, T + n_new, replay=graphs)
+                else:
+                    h = self._layers_step(h, i, pos0)
                 if info.last:
                     tok = self.model.head(h[:, -1:]).argmax(-1)  # [B, 1]
                     out[i, :, step] = tok[:, 0]
@@ -272,14 +336,15 @@ class PipelineRunner:
 
 
 @torch.no_grad()
-def greedy_generate(model, prompts, n_new):
+def greedy_generate(model, prompts, n_new, graphs=False, device_len=None):
     """The same greedy decoding in one process (world size 1): the reference's loop of
-    QuantLlamaDecoderLayer.forward with use_cache=True over a prompt, then one token at a time."""
+    QuantLlamaDecoderLayer.forward with use_cache=True over a prompt, then one token at a time
+    (``graphs`` / ``device_len``: see PipelineRunner.generate)."""
     info = StageInfo(0, 1, 0, len(model.layers))
     H = model.config.hidden_size
     runner = PipelineRunner(model, info, (1, 1, H), model.embed_tokens.weight.dtype,
                             model.embed_tokens.weight.device)
-    return runner.generate(prompts, n_new)
+    return runner.generate(prompts, n_new, graphs=graphs, device_len=device_len)
 
 
 def single_stage_nlls(model, windows):

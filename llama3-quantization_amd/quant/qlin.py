@@ -8,6 +8,7 @@ HIP stream (``torch.cuda`` is PyTorch-ROCm's native HIP backend).
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import threading
 import weakref
@@ -70,6 +71,8 @@ SIGNATURES = {
                           _p],
                          _i),
     "qlin_attn_decode_splits": ([_l, _i, _l], _i),
+    "qlin_attn_decode_rope_len": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _p, _i,
+                                   _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p, _p], _i),
 }
 
 
@@ -721,6 +724,43 @@ def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_
     rc = lib.qlin_attn_decode_rope(*args)
     _check(rc, "qlin_attn_decode_rope")
     return out
+
+
+def attn_decode_rope_len(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads,
+                         head_dim, k_cache, v_cache, length, out_dtype=torch.float32):
+    """``qlin_attn_decode_rope_len``: attn_decode_rope for graph-replayed decode steps — the cache
+    length (this step's new row + 1) is read from the int32 device tensor ``length`` [1], the
+    grid is sized for the caches' capacity (k_cache.shape[2] rows); no mask."""
+    for t_ in (q, k, v):
+        if _rows(t_) is None:
+            raise ValueError("attn_decode_rope_len takes row-strided [B, 1, H*D] q / k / v")
+    _on_gpu(q, k, v, cos_cache, sin_cache, position_ids, k_cache, v_cache, length)
+    B = q.shape[0]
+    if q.shape[1] != 1 or head_dim != ATTN_D or n_heads % n_kv_heads or \
+            n_heads // n_kv_heads not in (1, 2, 4, 8):
+        raise ValueError("attn_decode_rope_len: one token, head_dim 128, GQA group 1/2/4/8")
+    if length.dtype != torch.int32 or length.numel() < 1 or position_ids is None:
+        raise ValueError("attn_decode_rope_len: int32 length tensor and position_ids required")
+    if not (k_cache.is_contiguous() and v_cache.is_contiguous()) or k_cache.shape != v_cache.shape \
+            or tuple(k_cache.shape[:2]) != (B, n_kv_heads) or k_cache.shape[3] != head_dim:
+        raise ValueError("attn_decode_rope_len takes contiguous [B, Hkv, rows, D] caches")
+    cap = min(k_cache.shape[2], ATTN_MAX_L)
+    pos, pbs = _pos_ids(position_ids, B, 1)
+    out = torch.empty(B, n_heads, 1, head_dim, dtype=out_dtype, device=q.device)
+    lib = load_library()
+    part, cnt = _attn_partials(lib, q.device, B, n_heads, n_kv_heads, cap)
+    rc = lib.qlin_attn_decode_rope_len(
+        _ptr(q), _rows(q), _ptr(k), _rows(k), _ptr(v), _rows(v), _ptr(cos_cache), _ptr(sin_cache),
+        cos_cache.shape[0], _ptr(pos), pbs, _ptr(k_cache), _ptr(v_cache),
+        k_cache.shape[2] * head_dim, _ptr(out), _dtcode(out), B, n_heads, n_kv_heads, cap,
+        head_dim, ctypes.c_float(scale_div_default(head_dim)), _ptr(part), _ptr(cnt),
+        _ptr(length), _stream(q))
+    _check(rc, "qlin_attn_decode_rope_len")
+    return out
+
+
+def scale_div_default(head_dim):
+    return math.sqrt(head_dim)
 
 
 def attn_prefill_supported(q, k, mask=None):

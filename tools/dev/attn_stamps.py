@@ -17,7 +17,7 @@ lib = qlin.load_library()
 lib.qlin_dev_attn_stamps.argtypes = [ctypes.c_void_p]
 dev = torch.device("cuda:0")
 Hq, Hkv, D = 32, 8, 128
-NAMES = ["start", "q", "scores", "pv", "counted", "merge_in", "out"]
+NAMES = ["start", "q", "scores", "pv", "counted", "merge_in", "out", "softmax"]
 ONAMES = []
 
 

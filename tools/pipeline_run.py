@@ -39,7 +39,8 @@ def main():
     ap.add_argument("--fused", action="store_true",
                     help="packed + fuse_packed_projections() (fused q/k/v, gate/up+SiLU, epilogues)")
     ap.add_argument("--decode", type=int, default=0,
-                    help="also greedy-decode this many tokens for --micro sequences (decode "
+                    help="also greedy-decode this many tokens for --micro sequences, eager and "
+                         "with HIP-graph-replayed steps (decode "
                          "micro-batch mode: per-stage KV caches; fused layers use kv_cache=True)")
     ap.add_argument("--micro", type=int, default=0, help="decode sequences (default: world size)")
     ap.add_argument("--prompt", type=int, default=128, help="decode prompt length")
@@ -80,18 +81,29 @@ def main():
         prompts = [torch.randint(0, a.vocab, (1, a.prompt), device=dev, generator=g)
                    for _ in range(n_micro)] if info.first else None
         dr = PipelineRunner(model, info, (1, 1, a.hidden), torch.float16, dev)
-        dr.generate(prompts, 2)  # warm
-        torch.cuda.synchronize()
-        dist.barrier()
-        t1 = time.perf_counter()
-        toks = dr.generate(prompts, a.decode)
-        torch.cuda.synchronize()
-        dist.barrier()
-        dt_dec = time.perf_counter() - t1
-        dec = {"sequences": n_micro, "prompt": a.prompt, "new_tokens": a.decode,
-               "ms_per_step": round(dt_dec / a.decode * 1e3, 3),
-               "tokens_per_s": round(n_micro * a.decode / dt_dec, 1),
-               "first_tokens": toks[:, 0, :8].tolist()}
+
+        def timed(n, graphs):
+            torch.cuda.synchronize()
+            dist.barrier()
+            t1 = time.perf_counter()
+            toks = dr.generate(prompts, n, graphs=graphs)
+            torch.cuda.synchronize()
+            dist.barrier()
+            return time.perf_counter() - t1, toks
+
+        dec = {}
+        for mode, graphs in (("eager", False), ("graphs", True)):
+            timed(2, graphs)  # warm
+            short = max(2, a.decode // 4)
+            t_s, _ = timed(short, graphs)
+            t_l, toks = timed(a.decode, graphs)
+            # differential: the prefill step and the graph captures (first decode step of each
+            # sequence) cancel between the two runs
+            per_step = (t_l - t_s) / (a.decode - short)
+            dec[mode] = {"sequences": n_micro, "prompt": a.prompt, "new_tokens": a.decode,
+                         "ms_per_step": round(per_step * 1e3, 3),
+                         "tokens_per_s": round(n_micro / per_step, 1),
+                         "first_tokens": toks[:, 0, :8].tolist()}
     if rank == 0:
         ppl = float(torch.exp(nll.sum() / (a.windows * a.tokens)))
         print(json.dumps({"world": world, "layers": a.layers, "stages": [list(x) for x in
