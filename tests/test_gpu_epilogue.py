@@ -211,11 +211,12 @@ def test_attn_scores_pass_bit_exact(mask):
                                                (512, 1024, 2, 32, "residual"),
                                                (28672, 4096, 4, 128, "silu")])
 def test_rmsnorm_linear_matches_two_launches(N, K, bits, group, ep):
-    """qlin_rmsnorm_linear_ep_f16 (one token row: the GEMV multiplies RN16(w * x) and applies the
-    norm's rsqrt to its fp32 accumulators) against the two launches it replaces (qlin_rmsnorm_f16,
-    then the packed linear, which round w * (x * r) to fp16): the same mathematics with the fp16
-    rounding at another point — outputs within 2e-3 of max |y|, and no less accurate against a
-    float64 evaluation of the norm + linear on the same W_dq than the two launches."""
+    """qlin_rmsnorm_linear_ep_f16 (one token row: every block reduces the sum of squares, rounds
+    RN16(w * (x * r)) as the reference's norm output and multiplies that) against the two launches
+    it replaces (qlin_rmsnorm_f16, then the packed linear): the same rounding point, the sum of
+    squares in another fp32 order (an fp16 ulp of the normed x may move) — outputs within 2e-3 of
+    max |y|, and no less accurate against a float64 evaluation of the norm + linear on the same
+    W_dq than the two launches."""
     qw, qsz, fl = _packed(N, K, 21, bits, group)
     rs = np.random.RandomState(N + K)
     x = t((rs.randn(1, 1, K) * 3).astype(np.float16))
@@ -243,6 +244,30 @@ def test_rmsnorm_linear_matches_two_launches(N, K, bits, group, ep):
         y64 = y64 + res.double().reshape(-1)
     err = lambda a: (a.double().reshape(-1) - y64).abs().max().item()  # noqa: E731
     assert err(got) <= 1.25 * err(ref) + 1e-3 * scale, (err(got), err(ref))
+
+
+@pytest.mark.parametrize("xs,ws,outliers", [(1e-3, 1.0, False), (1e3, 1.0, True),
+                                            (1.0, 20.0, True), (30.0, 1.0, True)])
+def test_rmsnorm_linear_extreme_scales(xs, ws, outliers):
+    """The fused norm + linear where fp16 is tight: tiny inputs (normed values near the fp16
+    subnormals before the rsqrt), huge inputs with massive-activation channels, enlarged norm
+    weights (LET smoothing folds scales into them): finite and within 2e-3 of max |y| of the two
+    launches, whose rounding point (RN16(w * (x * r)), quant/omni_norm.py:54-63) it shares."""
+    N, K = 4096, 4096
+    qw, qsz, fl = _packed(N, K, 23, 4, 128)
+    rs = np.random.RandomState(7)
+    xv = rs.randn(K) * xs
+    if outliers:
+        xv[rs.choice(K, 6, replace=False)] *= 40.0
+    xv = np.clip(xv, -6e4, 6e4)
+    x = t(xv.astype(np.float16).reshape(1, 1, K))
+    w = torch.tensor(((1 + 0.1 * rs.randn(K)) * ws).astype(np.float32), device="cuda")
+    xn = qlin.rmsnorm(x, w, 1e-5)
+    ref = qlin.linear_ep(xn, qw, qsz, None, N, K, 4, 128, fl)
+    got = qlin.rmsnorm_linear_ep(x, w, 1e-5, qw, qsz, None, N, K, 4, 128, fl)
+    assert torch.isfinite(got).all() and torch.isfinite(ref).all()
+    scale = ref.float().abs().max().item()
+    assert (got.float() - ref.float()).abs().max().item() <= 2e-3 * scale
 
 
 def test_rmsnorm_linear_rejects_unsupported():
