@@ -43,11 +43,16 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kD = 128;          // head_dim
-constexpr int kThreads = 256;    // 4 waves
+#ifndef ATTN_THREADS  // dev A/B knob (tools/dev/Makefile.rows libattn_t<N>.so): 8 waves took
+#define ATTN_THREADS 256  // a cold launch 8.2 -> 7.6 us at L = 513 but the graph-replayed decode
+#endif                    // layer 43.25 -> 43.58 us (same box): 4 waves kept
+constexpr int kThreads = ATTN_THREADS;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxGroup = 8;     // query heads per KV head
 constexpr int kMaxL = 4096;
 constexpr int kSub = 64;         // positions per pass (8 lanes x 16 dims per K row)
+constexpr int kRowsU = kThreads / 8;  // K rows per load set (8 lanes per row)
+constexpr int kKU = kSub / kRowsU;    // load sets per pass
 constexpr int kMaxChunk = 512;   // scores of one chunk live in LDS: 512 x 8 fp32 = 16 KB
 constexpr int kMaxSplit = kMaxL / kSub;
 #ifndef ATTN_TARGET_BLOCKS  // dev sweeps (tools/dev/Makefile libattnT<N>.so); round 3: 256
@@ -266,12 +271,12 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   const _Float16* mb = mask ? mask + (int64_t)b * L + t0 : kb;
 
   // issue the first pass's K rows, V words and mask before anything waits
-  u32x4 kw[2][2];
-  float mv[2];
+  u32x4 kw[kKU][2];
+  float mv[kKU];
   auto load_k = [&](int tb) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int t = min(tb + 32 * u + tl, n - 1);
+    for (int u = 0; u < kKU; ++u) {
+      const int t = min(tb + kRowsU * u + tl, n - 1);
       const u32x4* kr = reinterpret_cast<const u32x4*>(kb + (int64_t)t * kD + 16 * sub);
       kw[u][0] = __builtin_nontemporal_load(kr);
       kw[u][1] = __builtin_nontemporal_load(kr + 1);
@@ -339,22 +344,22 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
 
   // scores (the next pass's K rows are in flight while this pass computes)
   for (int tb = 0; tb < n; tb += kSub) {
-    u32x4 kc[2][2];
-    float mc[2];
+    u32x4 kc[kKU][2];
+    float mc[kKU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kKU; ++u) {
       kc[u][0] = kw[u][0];
       kc[u][1] = kw[u][1];
       mc[u] = mv[u];
-      if (has_new && t0 + tb + 32 * u + tl == L - 1) {  // the new row: written by this launch
+      if (has_new && t0 + tb + kRowsU * u + tl == L - 1) {  // the new row: written by this launch
         kc[u][0] = *reinterpret_cast<const u32x4*>(&knew[16 * sub]);
         kc[u][1] = *reinterpret_cast<const u32x4*>(&knew[16 * sub + 8]);
       }
     }
     if (tb + kSub < n) load_k(tb + kSub);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int t = tb + 32 * u + tl;
+    for (int u = 0; u < kKU; ++u) {
+      const int t = tb + kRowsU * u + tl;
       float acc[GRP];
 #pragma unroll
       for (int g = 0; g < GRP; ++g) acc[g] = 0.f;
@@ -423,6 +428,10 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
 #pragma unroll
     for (int g = 0; g < GRP; ++g) a0[g] = a1[g] = 0.f;
     const uint32_t vn = has_new ? *reinterpret_cast<const uint32_t*>(&vnew[2 * lane]) : 0u;
+#if defined(ATTN_STAMP) && defined(ATTN_STAMP_VWAIT)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AT_STAMP(A, 5);  // dev: V landed (slot 5 is free in blocks that do not merge)
+#endif
     for (int tb = 0; tb < n; tb += kSub) {
       uint32_t vc[VR];
 #pragma unroll
@@ -464,13 +473,19 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
 
   const int64_t qh0 = (int64_t)b * Hq + (int64_t)hk * GRP;  // first query head of the group
   // output row of the group: fp32, or rounded once to fp16 (== the reference's .to(fp16))
+  auto wave_total = [&](int o) {  // the per-wave partials of element o, added in wave order
+    float r = po[0][o];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) r += po[w][o];
+    return r;
+  };
   auto put = [&](int o, float val) {
     if (out_f16) reinterpret_cast<_Float16*>(out)[qh0 * kD + o] = (_Float16)val;
     else reinterpret_cast<float*>(out)[qh0 * kD + o] = val;
   };
   auto put_all = [&]() {
     for (int o = tid; o < GRP * kD; o += kThreads)
-      put(o, (po[0][o] + po[1][o] + po[2][o] + po[3][o]) / cl[o / kD]);
+      put(o, wave_total(o) / cl[o / kD]);
     AT_STAMP(A, 6);
   };
   if (S == 1) {
@@ -481,7 +496,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   // write this chunk's partials, then count in; the last block of (b, kv head) merges
   float* pob = part_o + ((int64_t)bh * Sl + split) * GRP * kD;
   for (int o = tid; o < GRP * kD; o += kThreads)
-    part_store(pob + o, po[0][o] + po[1][o] + po[2][o] + po[3][o]);
+    part_store(pob + o, wave_total(o));
   if (tid < 2 * GRP) {
     float* ml = part_ml + ((int64_t)bh * Sl + split) * GRP * 2;
     part_store(ml + tid, (tid & 1) ? cl[tid >> 1] : cm[tid >> 1]);
@@ -502,7 +517,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   __threadfence();
 #endif
 
-  // merge: the first kPre partial rows of every wave (s = wave + 4 i) are requested together with
+  // merge: the first kPre partial rows of every wave (s = wave + kWaves i) are requested with
   // the chunk statistics — one memory round trip instead of two at decode lengths (S <= 16)
   constexpr int J = GRP * kD / 64;
   constexpr int kPre = GRP <= 4 ? 4 : 2;
@@ -542,7 +557,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     float acc[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[j] = 0.f;
-    // rows s = wave + 4 i, i < kPre, arrived with the statistics (same order as the loop below)
+    // rows s = wave + kWaves i, i < kPre, arrived with the statistics (same order as below)
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
       const int s = wave + kWaves * i;
