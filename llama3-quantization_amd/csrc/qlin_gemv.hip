@@ -674,10 +674,15 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
     }
   }
 
+  asm volatile("" ::: "memory");  // the x and norm-weight requests go out before the tiles'
+
   // the first PF tiles of the wave's first row (rows of PF-tile rounds: Kt % PF == 0)
   WTile<BITS, GPT> wt[PF];
   const int64_t wrow = (int64_t)a.Kt * (64 * BITS), srow = (int64_t)a.G * kTileN;
-  int64_t lr = gw;  // load cursor: row, k-tile
+  // load cursor: row, k-tile (a wave without rows reads row Nt - 1's first round, never used:
+  // the first round's loads stay unconditional, so the x staging below waits for the x words
+  // alone — behind a wave-uniform branch the join made hipcc wait for every tile, vmcnt(0))
+  int64_t lr = min<int64_t>(gw, a.Nt - 1);
   int lkt = 0;
   const uint32_t* lqw = a.qw + lr * wrow + lane * BITS;
   const uint32_t* lsz = a.qsz + lr * srow + n_in;
@@ -688,9 +693,17 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
 #pragma unroll
     for (int s = 0; s < GPT; ++s) wt[u].sz[s] = lsz[(g0 + s) * kTileN];
   };
-  if (nrow > 0) {  // wave-uniform
 #pragma unroll
-    for (int u = 0; u < PF; ++u) load(u);
+  for (int u = 0; u < PF; ++u) load(u);
+  // the x words count as produced here: their use (the statistics) is scheduled after every
+  // tile request above has been issued
+#pragma unroll
+  for (int i = 0; i < kWrowXIter; ++i) {
+    asm volatile("" : "+v"(xc[i].x), "+v"(xc[i].y), "+v"(xc[i].z), "+v"(xc[i].w)::"memory");
+    if constexpr (NRM)
+      asm volatile("" : "+v"(nc[2 * i].x), "+v"(nc[2 * i].y), "+v"(nc[2 * i].z),
+                   "+v"(nc[2 * i].w), "+v"(nc[2 * i + 1].x), "+v"(nc[2 * i + 1].y),
+                   "+v"(nc[2 * i + 1].z), "+v"(nc[2 * i + 1].w)::"memory");
   }
   ROWS_STAMP(1);
 
