@@ -118,6 +118,35 @@ def test_attn_decode_rope_equals_two_launches(B, Hq, Hkv, kv0, rows, masked):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("B,Hq,Hkv,kv0,cap", [(1, 32, 8, 512, 513), (1, 32, 8, 100, 1024),
+                                               (2, 16, 4, 77, 300), (1, 8, 1, 2000, 4096)])
+def test_attn_decode_rope_len_matches(B, Hq, Hkv, kv0, cap):
+    """qlin_attn_decode_rope_len (cache length read on the device, grid sized for the capacity):
+    at length == capacity bit-identical to qlin_attn_decode_rope, below it the same attention to
+    fp32 rounding (the rows split by the capacity's chunk); the new cache row written the same."""
+    from models.int_llama_layer import LlamaRotaryEmbedding437
+    D = 128
+    g = torch.Generator(device="cuda").manual_seed(kv0 + cap)
+    qkv = (torch.randn(B, 1, (Hq + 2 * Hkv) * D, device="cuda", generator=g) * 2).half()
+    q, k, v = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
+    rot = LlamaRotaryEmbedding437(D, 8192, 500000.0, device="cuda").half()
+    cos, sin = rot.cos_cached.float().contiguous(), rot.sin_cached.float().contiguous()
+    pos = torch.full((B, 1), kv0, device="cuda", dtype=torch.int64)
+    kc = torch.randn(B, Hkv, cap, D, device="cuda", generator=g).half()
+    vc = torch.randn(B, Hkv, cap, D, device="cuda", generator=g).half()
+    kc2, vc2 = kc.clone(), vc.clone()
+    length = torch.tensor([kv0 + 1], dtype=torch.int32, device="cuda")
+    got = qlin.attn_decode_rope_len(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, length)
+    ref = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc2, vc2, kv0, None,
+                                math.sqrt(D))
+    assert torch.equal(kc[:, :, :kv0 + 1], kc2[:, :, :kv0 + 1])
+    assert torch.equal(vc[:, :, :kv0 + 1], vc2[:, :, :kv0 + 1])
+    if kv0 + 1 == cap:
+        assert torch.equal(got, ref)
+    else:
+        assert (got - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
+
+
 def test_attn_decode_rejects_unsupported():
     q = torch.randn(1, 32, 1, 64, device="cuda")
     k = torch.randn(1, 8, 10, 64, device="cuda").half()
