@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 10
+#define QLIN_ABI_VERSION 11
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -54,6 +54,8 @@ extern "C" {
 /* packed-layout flags (dequant / GEMV / GEMM entry points) */
 #define QLIN_WIDE_ZERO          8
 #define QLIN_FLOAT_ZERO        16
+/* qlin_rmsnorm_linear_ep_f16: the norm weight is fp16 (the module's own), not fp32 */
+#define QLIN_NORM_W16          32
 
 /* return codes (hipError_t values; anything else is a HIP error passed through) */
 #define QLIN_OK     0
@@ -223,8 +225,9 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
  * RMSNorm + packed linear for ONE token row in one launch (the decoder layer's
  * input_layernorm -> fused q/k/v and post_attention_layernorm -> gate/up at decode; the norm is
  * OmniLlamaRMSNorm, quant/omni_norm.py:52-63 of the reference): x fp16 [K] is the hidden state
- * BEFORE the norm, norm_weight fp32 [K] (8-B aligned; the fp16 weight upcast, exact), eps its
- * variance epsilon.  The kernel normalises x at the reference's rounding point,
+ * BEFORE the norm, norm_weight [K]: fp32 (8-B aligned; the fp16 weight upcast, exact) or, with
+ * flags & QLIN_NORM_W16, the fp16 weight itself (4-B aligned; half the bytes, same result), eps
+ * its variance epsilon.  The kernel normalises x at the reference's rounding point,
  * x_hat = RN16(weight * (x * rsqrt(mean(x^2) + eps))) with fp32 inside, and multiplies x_hat:
  * y = F.linear(x_hat, W_dq, bias), then `epilogue` as qlin_linear_ep_f16.  The sum of squares runs
  * in another order than torch's reduction (an fp32 ulp of the statistics can move an fp16 ulp of
@@ -234,7 +237,7 @@ int qlin_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, 
  */
 int qlin_rmsnorm_linear_supported(int64_t M, int64_t N, int64_t K, int bits, int group);
 int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
-                               const uint16_t* x, const float* norm_weight, float eps,
+                               const uint16_t* x, const void* norm_weight, float eps,
                                const uint16_t* bias, const uint16_t* residual, uint16_t* y,
                                int64_t M, int64_t N, int64_t K, int bits, int group, int epilogue,
                                void* stream);

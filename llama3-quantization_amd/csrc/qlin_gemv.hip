@@ -385,6 +385,27 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
 #endif
 constexpr int kRowsMaxTPW = 8;  // k-tiles per wave and row
 
+// NRM (the fused RMSNorm of one token row): 0 none, kNwF32 an fp32 norm weight, kNwF16 the
+// module's fp16 weight (half the bytes; every fp16 is exact in fp32, so the normed x is the same)
+constexpr int kNwF32 = 1, kNwF16 = 2;
+// two norm weights (k, k + 1) as loaded: raw until used, so no wait is scheduled at the load
+template <int NRM>
+using NwPair = std::conditional_t<NRM == kNwF16, uint32_t, float2>;
+template <int NRM>
+__device__ __forceinline__ NwPair<NRM> load_nw_pair(const void* nw, int k) {
+  if constexpr (NRM == kNwF16) return *reinterpret_cast<const uint32_t*>((const _Float16*)nw + k);
+  else return *reinterpret_cast<const float2*>((const float*)nw + k);
+}
+template <int NRM>
+__device__ __forceinline__ float2 nw_pair_f32(NwPair<NRM> w) {
+  if constexpr (NRM == kNwF16) {
+    const h2 v = as_h2(w);
+    return float2{(float)v.x, (float)v.y};
+  } else {
+    return w;
+  }
+}
+
 struct RowsArgs {
   const uint32_t* qw;   // tile row 0 of qweight
   const uint32_t* qsz;  // tile row 0 of qsz
@@ -392,7 +413,7 @@ struct RowsArgs {
   const _Float16* bias;
   const _Float16* res;  // kEpResidual
   _Float16* y;
-  const float* nw;      // NRM: RMSNorm weight, fp32 [K]
+  const void* nw;       // NRM: RMSNorm weight [K], fp32 or fp16 (kNwF32 / kNwF16)
   float eps;
   int ep, has_bias;     // bias / res always readable (the host points absent ones at y)
   int64_t nres;         // readable elements at res
@@ -414,7 +435,7 @@ inline uint64_t* g_rows_stamps = nullptr;  // set by qlin_dev_rows_stamps (dev b
 #define ROWS_STAMP(k)
 #endif
 
-template <int BITS, int GPT, int ZM, int TPW, int PF, bool NRM>
+template <int BITS, int GPT, int ZM, int TPW, int PF, int NRM>
 __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][TPW * 64];  // the wave's x words
   __shared__ __attribute__((aligned(16))) float red[2][kTileN][kMaxWaves];   // row partials
@@ -437,13 +458,13 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
   // issued first (in-order completion: their wait does not wait for the weights)
   const _Float16* xp = a.x + kt0 * kTileK + 2 * lane;
   uint32_t xw[TPW];
-  float2 nwv[NRM ? TPW : 1];
+  NwPair<NRM> nwv[NRM ? TPW : 1];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) xw[i] = *reinterpret_cast<const uint32_t*>(xp + i * kts * kTileK);
   if constexpr (NRM) {
-    const float* np = a.nw + kt0 * kTileK + 2 * lane;
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) nwv[i] = *reinterpret_cast<const float2*>(np + i * kts * kTileK);
+    for (int i = 0; i < TPW; ++i)
+      nwv[i] = load_nw_pair<NRM>(a.nw, (kt0 + i * kts) * kTileK + 2 * lane);
   }
 
   // the epilogue operands of the first row this wave finishes (the epilogue of a block's j-th row
@@ -511,8 +532,9 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const h2 v = as_h2(xw[i]);
-      const float n0 = nwv[i].x * ((float)v.x * rn);
-      const float n1 = nwv[i].y * ((float)v.y * rn);
+      const float2 w = nw_pair_f32<NRM>(nwv[i]);
+      const float n0 = w.x * ((float)v.x * rn);
+      const float n1 = w.y * ((float)v.y * rn);
       xw[i] = as_u32(h2{(_Float16)n0, (_Float16)n1});
     }
   }
@@ -633,7 +655,7 @@ struct WrowArgs {
   const _Float16* bias;
   const _Float16* res;
   _Float16* y;
-  const float* nw;      // NRM: RMSNorm weight fp32 [K]
+  const void* nw;       // NRM: RMSNorm weight [K], fp32 or fp16 (kNwF32 / kNwF16)
   float eps;
   int ep, has_bias;     // bias / res always readable (the host points absent ones at y)
   int64_t nres;         // readable elements at res
@@ -645,7 +667,7 @@ struct WrowArgs {
 #endif
 };
 
-template <int BITS, int GPT, int ZM, int PF, bool NRM>
+template <int BITS, int GPT, int ZM, int PF, int NRM>
 __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const WrowArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 xs4[];  // x (normed), fp16 [K]: K / 8 chunks
   __shared__ float nss[kWrowMaxWaves];
@@ -663,12 +685,15 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
   // x chunks of this thread (clamped: repeats are never stored), issued first
   const int nch = a.K >> 3;
   uint4 xc[kWrowXIter];
+  // the chunk's 8 norm weights: two float4 (fp32) or one uint4 of fp16 (kNwF16: nc[2i + 1] unused)
   float4 nc[NRM ? 2 * kWrowXIter : 1];
 #pragma unroll
   for (int i = 0; i < kWrowXIter; ++i) {
     const int c = min(tid + i * nthr, nch - 1);
     xc[i] = reinterpret_cast<const uint4*>(a.x)[c];
-    if constexpr (NRM) {
+    if constexpr (NRM == kNwF16) {
+      nc[2 * i] = __builtin_bit_cast(float4, reinterpret_cast<const uint4*>(a.nw)[c]);
+    } else if constexpr (NRM) {
       nc[2 * i] = reinterpret_cast<const float4*>(a.nw)[2 * c];
       nc[2 * i + 1] = reinterpret_cast<const float4*>(a.nw)[2 * c + 1];
     }
@@ -700,7 +725,10 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
 #pragma unroll
   for (int i = 0; i < kWrowXIter; ++i) {
     asm volatile("" : "+v"(xc[i].x), "+v"(xc[i].y), "+v"(xc[i].z), "+v"(xc[i].w)::"memory");
-    if constexpr (NRM)
+    if constexpr (NRM == kNwF16)
+      asm volatile("" : "+v"(nc[2 * i].x), "+v"(nc[2 * i].y), "+v"(nc[2 * i].z),
+                   "+v"(nc[2 * i].w)::"memory");
+    else if constexpr (NRM)
       asm volatile("" : "+v"(nc[2 * i].x), "+v"(nc[2 * i].y), "+v"(nc[2 * i].z),
                    "+v"(nc[2 * i].w), "+v"(nc[2 * i + 1].x), "+v"(nc[2 * i + 1].y),
                    "+v"(nc[2 * i + 1].z), "+v"(nc[2 * i + 1].w)::"memory");
@@ -728,8 +756,17 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
 #pragma unroll
     for (int i = 0; i < kWrowXIter; ++i) {
       const h8 v = __builtin_bit_cast(h8, xc[i]);
-      const float w8[8] = {nc[2 * i].x, nc[2 * i].y, nc[2 * i].z, nc[2 * i].w,
-                           nc[2 * i + 1].x, nc[2 * i + 1].y, nc[2 * i + 1].z, nc[2 * i + 1].w};
+      float w8[8];
+      if constexpr (NRM == kNwF16) {
+        const h8 h = __builtin_bit_cast(h8, nc[2 * i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w8[j] = (float)h[j];
+      } else {
+        const float t8[8] = {nc[2 * i].x, nc[2 * i].y, nc[2 * i].z, nc[2 * i].w,
+                             nc[2 * i + 1].x, nc[2 * i + 1].y, nc[2 * i + 1].z, nc[2 * i + 1].w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w8[j] = t8[j];
+      }
       h8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (_Float16)(w8[j] * ((float)v[j] * rn));
@@ -852,11 +889,11 @@ struct FastArgs {
   int M, N, K, Kt, G;
   int W, lw;            // waves per block (power of two), log2 W
   uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
-  const float* nw;      // NRM: RMSNorm weight (fp32 [K]) applied to x first
+  const void* nw;       // NRM: RMSNorm weight [K] (fp32 / fp16) applied to x first
   float eps;
 };
 
-template <int BITS, int MT, int GPT, int ZM, int EP, int PF, bool NRM = false>
+template <int BITS, int MT, int GPT, int ZM, int EP, int PF, int NRM = 0>
 __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   __shared__ __attribute__((aligned(16))) float red[MT * kTileN * kMaxWaves];
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMaxWaves][64 * MT];
@@ -881,7 +918,7 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
   };
   WTile<BITS, GPT> wt[PF];
   XRaw<MT> xq[PF];
-  float2 nwv[NRM ? PF : 1];  // NRM: norm weights of the lane's two x halves per tile
+  NwPair<NRM> nwv[NRM ? PF : 1];  // NRM: norm weights of the lane's two x halves per tile
   auto load_codes = [&](int u, int kt) { wt[u].pc = load_piece_nt<BITS>(qw + kt * (64 * BITS)); };
   auto load_sz = [&](int u, int kt) {
     const int g0 = group_of_tile(kt);
@@ -904,7 +941,7 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       load_x(u, kt_of(u));
-      nwv[u] = *reinterpret_cast<const float2*>(a.nw + kt_of(u) * kTileK + 2 * lane);
+      nwv[u] = load_nw_pair<NRM>(a.nw, kt_of(u) * kTileK + 2 * lane);
     }
 #pragma unroll
     for (int u = 0; u < PF; ++u) load_codes(u, kt_of(u));
@@ -963,8 +1000,9 @@ __global__ __launch_bounds__(1024) void gemv_fast_kernel(const FastArgs a) {
     if constexpr (NRM) {
 #pragma clang fp contract(off)
       const h2 v = as_h2(xq[u].w[0]);
-      const float n0 = nwv[u].x * ((float)v.x * rn);
-      const float n1 = nwv[u].y * ((float)v.y * rn);
+      const float2 w = nw_pair_f32<NRM>(nwv[u]);
+      const float n0 = w.x * ((float)v.x * rn);
+      const float n1 = w.y * ((float)v.y * rn);
       xq[u].w[0] = as_u32(h2{(_Float16)n0, (_Float16)n1});
     }
     park_x<MT>(xa, xq[u], slot, lane, n_in);
@@ -1141,7 +1179,7 @@ static inline bool wrow_geometry(int64_t Nt, int Kt, int K, WrowGeo& g) {
   return (int64_t)g.rw * 64 * kWrowXIter * 8 >= K;
 }
 
-template <int BITS, int GPT, int ZM, bool NRM>
+template <int BITS, int GPT, int ZM, int NRM>
 int launch_wrow(const WrowArgs& a, const WrowGeo& g, hipStream_t st) {
   const size_t lds = (size_t)a.K * 2;
 #define QLIN_WR(P)                                                                             \
@@ -1156,7 +1194,7 @@ int launch_wrow(const WrowArgs& a, const WrowGeo& g, hipStream_t st) {
 template <int BITS, int ZM>
 int launch_wrow_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int N, int K, int group, hipStream_t st, int ep,
-                  const uint16_t* res, const float* nw, float eps, const WrowGeo& g) {
+                  const uint16_t* res, const void* nw, bool nw16, float eps, const WrowGeo& g) {
   WrowArgs a;
 #ifdef GEMV_ROWS_STAMP
   a.stamps = g_rows_stamps;
@@ -1180,7 +1218,9 @@ int launch_wrow_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   a.nwaves = g.nb * g.rw;
   a.cmagic = tile_group_magic(group);
 #define QLIN_WG(GPT)                                                                            \
-  return nw ? launch_wrow<BITS, GPT, ZM, true>(a, g, st) : launch_wrow<BITS, GPT, ZM, false>(a, g, st)
+  return !nw  ? launch_wrow<BITS, GPT, ZM, 0>(a, g, st)                                         \
+         : nw16 ? launch_wrow<BITS, GPT, ZM, kNwF16>(a, g, st)                                  \
+                : launch_wrow<BITS, GPT, ZM, kNwF32>(a, g, st)
   if (group % kTileK == 0) QLIN_WG(1);
   if (group == 64) QLIN_WG(2);
   QLIN_WG(4);
@@ -1222,7 +1262,7 @@ static inline bool rows_geometry(int64_t Nt, int Kt, RowsGeo& g) {
 }
 
 
-template <int BITS, int GPT, int ZM, bool NRM>
+template <int BITS, int GPT, int ZM, int NRM>
 int launch_rows(const RowsArgs& a, const RowsGeo& g, hipStream_t st) {
   size_t lds = 0;
   if (g.nb < a.N / kTileN && GEMV_ROWS_LDS_MIN > 0) lds = GEMV_ROWS_LDS_MIN;
@@ -1245,7 +1285,7 @@ int launch_rows(const RowsArgs& a, const RowsGeo& g, hipStream_t st) {
 template <int BITS, int ZM>
 int launch_rows_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int N, int K, int group, hipStream_t st, int ep,
-                  const uint16_t* res, const float* nw, float eps, const RowsGeo& g) {
+                  const uint16_t* res, const void* nw, bool nw16, float eps, const RowsGeo& g) {
   const int64_t Nt = (N + kTileN - 1) / kTileN;
   RowsArgs a;
   a.qw = qw;
@@ -1276,7 +1316,9 @@ int launch_rows_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   a.stamps = g_rows_stamps;
 #endif
 #define QLIN_RG(GPT)                                                                            \
-  return nw ? launch_rows<BITS, GPT, ZM, true>(a, g, st) : launch_rows<BITS, GPT, ZM, false>(a, g, st)
+  return !nw  ? launch_rows<BITS, GPT, ZM, 0>(a, g, st)                                         \
+         : nw16 ? launch_rows<BITS, GPT, ZM, kNwF16>(a, g, st)                                  \
+                : launch_rows<BITS, GPT, ZM, kNwF32>(a, g, st)
   if (group % kTileK == 0) QLIN_RG(1);
   if (group == 64) QLIN_RG(2);
   QLIN_RG(4);
@@ -1285,19 +1327,24 @@ int launch_rows_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
 
 // ---- M <= 4: the fast kernel -----------------------------------------------------------------
 template <int BITS, int MT, int GPT, int ZM, int EP>
-int launch_fast_t(const FastArgs& a, int Nt, int tpw, hipStream_t st) {
+int launch_fast_t(const FastArgs& a, bool nw16, int Nt, int tpw, hipStream_t st) {
 #define QLIN_GF(PF, NR)                                                                      \
   hipLaunchKernelGGL((gemv_fast_kernel<BITS, MT, GPT, ZM, EP, PF, NR>), dim3(Nt),          \
                      dim3(64 * a.W), 0, st, a)
   if constexpr (MT == 1) {
+    if (a.nw && nw16) {
+      if (tpw <= 2) QLIN_GF(2, kNwF16);
+      else QLIN_GF(4, kNwF16);
+      return (int)hipGetLastError();
+    }
     if (a.nw) {
-      if (tpw <= 2) QLIN_GF(2, true);
-      else QLIN_GF(4, true);
+      if (tpw <= 2) QLIN_GF(2, kNwF32);
+      else QLIN_GF(4, kNwF32);
       return (int)hipGetLastError();
     }
   }
-  if (tpw <= 2) QLIN_GF(2, false);
-  else QLIN_GF(4, false);
+  if (tpw <= 2) QLIN_GF(2, 0);
+  else QLIN_GF(4, 0);
 #undef QLIN_GF
   return (int)hipGetLastError();
 }
@@ -1325,8 +1372,8 @@ static inline bool fast_ok(int M, int K, int group, const Ep& e) {
 template <int BITS, int MT, int ZM>
 int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                 uint16_t* y, int M, int N, int K, int group, int W, int lw, int tpw,
-                hipStream_t st, int ep, const uint16_t* res, const float* nw = nullptr,
-                float eps = 0.f) {
+                hipStream_t st, int ep, const uint16_t* res, const void* nw = nullptr,
+                bool nw16 = false, float eps = 0.f) {
   const int Nt = (N + kTileN - 1) / kTileN;
   FastArgs a;
   a.qw = qw;
@@ -1346,9 +1393,9 @@ int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
   a.nw = nw;
   a.eps = eps;
 #define QLIN_FE(GPT)                                                                           \
-  return ep == kEpResidual  ? launch_fast_t<BITS, MT, GPT, ZM, kEpResidual>(a, Nt, tpw, st)  \
-         : ep == kEpSiluMul ? launch_fast_t<BITS, MT, GPT, ZM, kEpSiluMul>(a, Nt, tpw, st)   \
-                            : launch_fast_t<BITS, MT, GPT, ZM, kEpNone>(a, Nt, tpw, st)
+  return ep == kEpResidual  ? launch_fast_t<BITS, MT, GPT, ZM, kEpResidual>(a, nw16, Nt, tpw, st)  \
+         : ep == kEpSiluMul ? launch_fast_t<BITS, MT, GPT, ZM, kEpSiluMul>(a, nw16, Nt, tpw, st)   \
+                            : launch_fast_t<BITS, MT, GPT, ZM, kEpNone>(a, nw16, Nt, tpw, st)
   if (group % kTileK == 0) QLIN_FE(1);
   if (group == 64) QLIN_FE(2);
   QLIN_FE(4);
@@ -1360,7 +1407,7 @@ int launch_fast(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, cons
 // down 4,096 x 14,336 rows 8.25 us vs gemv_kernel 8.7; 4096^2 and q/k/v fast 3.7 / 5.7 us vs rows
 // 3.8-4.2 / 6.1)
 enum { kM1None = 0, kM1Wrow, kM1Fast, kM1Rows };
-static inline int m1_route(int64_t N, int K, int group, const void* x, const float* nw, WrowGeo& wg,
+static inline int m1_route(int64_t N, int K, int group, const void* x, const void* nw, WrowGeo& wg,
                            int& W, int& lw, int& tpw, RowsGeo& rg) {
   if (!group_fast(K, group)) return kM1None;
   const int64_t Nt = (N + kTileN - 1) / kTileN;
@@ -1375,18 +1422,20 @@ static inline int m1_route(int64_t N, int K, int group, const void* x, const flo
 template <int BITS, int ZM>
 int launch_m1(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
               uint16_t* y, int N, int K, int group, hipStream_t st, int ep, const uint16_t* res,
-              const float* nw, float eps) {
+              const void* nw, bool nw16, float eps) {
   WrowGeo wg;
   RowsGeo rg;
   int W = 0, lw = 0, tpw = 0;
   switch (m1_route(N, K, group, x, nw, wg, W, lw, tpw, rg)) {
     case kM1Wrow:
-      return launch_wrow_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, ep, res, nw, eps, wg);
+      return launch_wrow_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, ep, res, nw, nw16, eps,
+                                      wg);
     case kM1Fast:
       return launch_fast<BITS, 1, ZM>(qw, qsz, x, bias, y, 1, N, K, group, W, lw, tpw, st, ep,
-                                      res, nw, eps);
+                                      res, nw, nw16, eps);
     case kM1Rows:
-      return launch_rows_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, ep, res, nw, eps, rg);
+      return launch_rows_g<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, ep, res, nw, nw16, eps,
+                                      rg);
     default:
       return QLIN_EINVAL;
   }
@@ -1410,7 +1459,8 @@ int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
     RowsGeo rg;
     int W = 0, lw = 0, tpw = 0;
     if (m1_route(N, K, group, x, nullptr, wg, W, lw, tpw, rg) != kM1None)
-      return launch_m1<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, e.ep, e.res, nullptr, 0.f);
+      return launch_m1<BITS, ZM>(qw, qsz, x, bias, y, N, K, group, st, e.ep, e.res, nullptr, false,
+                                 0.f);
   }
   int W = 0, lw = 0, tpw = 0;
   if (M > 1 && fast_ok(M, K, group, e) &&
@@ -1437,8 +1487,8 @@ int launch_gemv_m(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
                                                 hipStream_t, const qlin_gv::Ep&);                \
   EXT template int qlin_gv::launch_m1<B, Z>(const uint32_t*, const uint32_t*, const uint16_t*,  \
                                             const uint16_t*, uint16_t*, int, int, int,           \
-                                            hipStream_t, int, const uint16_t*, const float*,     \
-                                            float)
+                                            hipStream_t, int, const uint16_t*, const void*,      \
+                                            bool, float)
 #define QLIN_GV_INST_B(EXT, B)           \
   QLIN_GV_INST(EXT, B, kZNarrow);        \
   QLIN_GV_INST(EXT, B, kZWide);          \
@@ -1530,12 +1580,13 @@ extern "C" int qlin_rmsnorm_linear_supported(int64_t M, int64_t N, int64_t K, in
 }
 
 extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
-                                          const uint16_t* x, const float* norm_weight, float eps,
+                                          const uint16_t* x, const void* norm_weight, float eps,
                                           const uint16_t* bias, const uint16_t* residual,
                                           uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
                                           int group, int epilogue, void* stream) {
+  const bool nw16 = (flags & QLIN_NORM_W16) != 0;
   if (!qweight || !qsz || !x || !norm_weight || !y || !rmsnorm_linear_ok(M, N, K, bits, group) ||
-      ((uintptr_t)norm_weight & 7) || ((uintptr_t)x & 3) || !(eps >= 0.f) ||
+      ((uintptr_t)norm_weight & (nw16 ? 3 : 7)) || ((uintptr_t)x & 3) || !(eps >= 0.f) ||
       epilogue < kEpNone || epilogue > kEpSiluMul || (epilogue == kEpResidual && !residual) ||
       (epilogue == kEpSiluMul && N % kTileN))
     return QLIN_EINVAL;
@@ -1544,11 +1595,11 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
   const int zm = zero_mode(flags);
 #define QLIN_N(B)                                                                              \
   return zm == kZFloat ? launch_m1<B, kZFloat>(qweight, qsz, x, bias, y, n, k, group, st,  \
-                                               epilogue, residual, norm_weight, eps)       \
+                                               epilogue, residual, norm_weight, nw16, eps)       \
          : zm == kZWide ? launch_m1<B, kZWide>(qweight, qsz, x, bias, y, n, k, group, st,  \
-                                               epilogue, residual, norm_weight, eps)       \
+                                               epilogue, residual, norm_weight, nw16, eps)       \
                         : launch_m1<B, kZNarrow>(qweight, qsz, x, bias, y, n, k, group, st, \
-                                                 epilogue, residual, norm_weight, eps)
+                                                 epilogue, residual, norm_weight, nw16, eps)
   switch (bits) {
     case 2: QLIN_N(2);
     case 3: QLIN_N(3);

@@ -62,11 +62,16 @@ class OmniLlamaRMSNorm(nn.Module):
         return self._w32[2]
 
     def fusable(self, hidden_states):
-        """(fp32 weight, eps) when the next packed linear may apply this norm itself
-        (qlin.rmsnorm_linear_ep: the kernel path, one fp16 token row), else None."""
+        """(weight, eps) when the next packed linear may apply this norm itself
+        (qlin.rmsnorm_linear_ep: the kernel path, one fp16 token row), else None.  An fp16 module
+        weight goes as it is (the kernel reads fp16 weights: half the bytes, same result), any
+        other as its fp32 copy."""
         if (self.use_kernel and not self.use_temporary_parameter and self.bias is None
                 and hidden_states.is_cuda and hidden_states.dtype == torch.float16
                 and hidden_states.numel() == hidden_states.shape[-1]):
+            w = self.weight
+            if w.dtype == torch.float16 and w.is_contiguous():
+                return w.detach(), self.variance_epsilon
             return self._kernel_weight(), self.variance_epsilon
         return None
 

@@ -18,13 +18,14 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
 LWC = 4
 WIDE_ZERO = 8
 FLOAT_ZERO = 16
+NORM_W16 = 32  # rmsnorm_linear_ep: fp16 norm weight
 F16 = 0
 F32 = 1
 
@@ -423,10 +424,15 @@ def rmsnorm_linear_ep(x, norm_weight, eps, qweight, qsz, bias, N, K, bits, group
     x fp16 [.., K] is the hidden state BEFORE the RMSNorm (norm_weight fp32 [K], eps), which the
     kernel applies at the reference's rounding point, RN16(w * (x * rsqrt(mean(x^2) + eps)))
     (the sum of squares in another order than ``rmsnorm``: an fp16 ulp of the normed x can
-    differ from it)."""
+    differ from it).  An fp16 norm weight is read as fp16 (QLIN_NORM_W16: half the bytes; every
+    fp16 is exact in fp32, so the result is the one of its fp32 copy)."""
     _dev(x, qweight, qsz, bias, residual, norm_weight)
-    if x.dtype != torch.float16 or norm_weight.dtype != torch.float32:
-        raise ValueError("rmsnorm_linear_ep takes fp16 x and an fp32 norm weight")
+    if x.dtype != torch.float16 or norm_weight.dtype not in (torch.float32, torch.float16):
+        raise ValueError("rmsnorm_linear_ep takes fp16 x and an fp32 or fp16 norm weight")
+    if not norm_weight.is_contiguous():
+        raise ValueError("norm weight must be contiguous")
+    if norm_weight.dtype == torch.float16:
+        flags |= NORM_W16
     if x.shape[-1] != K or norm_weight.numel() != K:
         raise ValueError(f"input / norm weight do not have {K} features")
     if bias is not None and (bias.dtype != torch.float16 or bias.numel() != N):

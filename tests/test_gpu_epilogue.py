@@ -270,6 +270,32 @@ def test_rmsnorm_linear_extreme_scales(xs, ws, outliers):
     assert (got.float() - ref.float()).abs().max().item() <= 2e-3 * scale
 
 
+@pytest.mark.parametrize("N,K,bits,group,ep,offset", [(28672, 4096, 4, 128, "silu", 0),   # whole-row
+                                                      (28672, 4096, 4, 128, "silu", 2),   # unaligned
+                                                      (6144, 4096, 4, 128, "none", 0),    # fast
+                                                      (4096, 14336, 4, 128, "residual", 0),  # rows
+                                                      (512, 1024, 2, 32, "residual", 0),
+                                                      (1024, 2048, 3, 64, "none", 0)])
+def test_rmsnorm_linear_fp16_norm_weight(N, K, bits, group, ep, offset):
+    """QLIN_NORM_W16: the module's fp16 norm weight read as fp16 gives the output of its fp32 copy
+    bit for bit on every M = 1 route (the whole-row, fast and rows kernels; a weight only 4-B
+    aligned leaves the whole-row kernel, which reads 16-B chunks)."""
+    qw, qsz, fl = _packed(N, K, 29, bits, group)
+    rs = np.random.RandomState(N + K + offset)
+    x = t((rs.randn(1, 1, K) * 3).astype(np.float16))
+    w16 = torch.tensor((1 + 0.1 * rs.randn(K + offset)).astype(np.float16), device="cuda")[offset:]
+    epc = {"none": qlin.EP_NONE, "residual": qlin.EP_RESIDUAL, "silu": qlin.EP_SILU_MUL}[ep]
+    ny = N // 2 if ep == "silu" else N
+    res = t(rs.randn(1, 1, ny).astype(np.float16)) if ep == "residual" else None
+    # the fp32 copy at the same offset (8-B aligned at offset 2): the same route as w16
+    w32 = torch.cat([torch.zeros(offset, device="cuda"), w16.float()])[offset:]
+    ref = qlin.rmsnorm_linear_ep(x, w32, 1e-5, qw, qsz, None, N, K, bits, group, fl,
+                                 epilogue=epc, residual=res)
+    got = qlin.rmsnorm_linear_ep(x, w16, 1e-5, qw, qsz, None, N, K, bits, group, fl,
+                                 epilogue=epc, residual=res)
+    assert torch.equal(got, ref)
+
+
 def test_rmsnorm_linear_rejects_unsupported():
     qw, qsz, fl = _packed(256, 1024, 5)
     w = torch.ones(1024, device="cuda")

@@ -1,7 +1,8 @@
 """Dev: the decode layer's four linear launches (M = 1, int4 g128) under library variants, each a HIP
 graph of dependent launches over a ring of distinct matrices (> 600 MB per shape, beyond the
 MALL).  Usage: rows_sweep.py lib1.so [lib2.so ...]; a library named libr3*.so is called with the
-round-3 (ABI 9) signature of qlin_rmsnorm_linear_ep_f16."""
+round-3 (ABI 9) signature of qlin_rmsnorm_linear_ep_f16; lib.so@w16 is lib.so with the norm weight
+in fp16 (QLIN_NORM_W16)."""
 import ctypes
 import os
 import sys
@@ -13,8 +14,15 @@ from quant import qlin  # noqa: E402
 
 dev = torch.device("cuda:0")
 P, L64, F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_float
-libs = [(os.path.basename(nm), ctypes.CDLL(nm if "/" in nm else os.path.join(ROOT, "tools/dev", nm)))
-        for nm in sys.argv[1:]]
+
+def _open(nm):
+    f = nm.split("@")[0]
+    if f == "libqlin_gfx950.so" and "/" not in f:
+        f = os.path.join(ROOT, "llama3-quantization_amd/csrc", f)
+    return ctypes.CDLL(f if "/" in f else os.path.join(ROOT, "tools/dev", f))
+
+
+libs = [(os.path.basename(nm), _open(nm)) for nm in sys.argv[1:]]
 # (name, N, K, epilogue, fused RMSNorm)
 SHAPES = [("qkv+norm", 6144, 4096, qlin.EP_NONE, True), ("o+res", 4096, 4096, qlin.EP_RESIDUAL, False),
           ("gateup+norm+silu", 28672, 4096, qlin.EP_SILU_MUL, True),
@@ -31,13 +39,15 @@ for (name, N, K, ep, nrm) in SHAPES:
         mats.append((o["qweight"], o["qsz"]))
         del w
     x = torch.randn(1, K, device=dev, dtype=torch.float16)
-    nw = (1 + 0.1 * torch.randn(K, device=dev)).float()
+    nw16 = (1 + 0.1 * torch.randn(K, device=dev)).half()
+    nw = nw16.float()
     ny = N // 2 if ep == qlin.EP_SILU_MUL else N
     y = torch.empty(1, ny, device=dev, dtype=torch.float16)
     r = torch.randn(1, ny, device=dev, dtype=torch.float16)
     res, outs = {}, {}
     for nm, lib in libs:
         r3 = nm.startswith("libr3")
+        w16 = nm.endswith("@w16")
 
         def step():
             st = P(torch.cuda.current_stream().cuda_stream)
@@ -45,7 +55,8 @@ for (name, N, K, ep, nrm) in SHAPES:
                 if nrm:
                     extra = (None, L64(0), None, None, None, L64(0), None) if r3 else ()
                     rc = lib.qlin_rmsnorm_linear_ep_f16(
-                        P(qw.data_ptr()), P(qsz.data_ptr()), 0, P(x.data_ptr()), P(nw.data_ptr()),
+                        P(qw.data_ptr()), P(qsz.data_ptr()), qlin.NORM_W16 if w16 else 0,
+                        P(x.data_ptr()), P((nw16 if w16 else nw).data_ptr()),
                         F(1e-5), None, None, P(y.data_ptr()), L64(1), L64(N), L64(K), 4, 128, ep,
                         *extra, st)
                 else:
