@@ -1160,6 +1160,9 @@ static inline bool group_fast(int K, int group) {  // whole-tile or 32 / 64-wide
 #ifndef GEMV_WROW_MIN_ROWS_CU  // dev knob: tile rows per CU from which the whole-row kernel runs
 #define GEMV_WROW_MIN_ROWS_CU 4
 #endif
+#ifndef GEMV_WROW_RW  // dev knob: waves (rows in flight) per block; 0 = ceil(rows / CUs)
+#define GEMV_WROW_RW 0
+#endif
 #ifndef GEMV_WROW_PF  // dev knob: tiles in flight per wave (gate/up: 8 15.3 us, 16 17.2 us;
 #define GEMV_WROW_PF 8  // tools/dev/rows_sweep.py, one box)
 #endif
@@ -1173,7 +1176,7 @@ static inline bool wrow_geometry(int64_t Nt, int Kt, int K, WrowGeo& g) {
   if (Nt < GEMV_WROW_MIN_ROWS_CU * cus) return false;
   g.pf = Kt % GEMV_WROW_PF == 0 ? GEMV_WROW_PF : (Kt % 8 == 0 ? 8 : 0);
   if (!g.pf) return false;
-  g.rw = (int)std::min<int64_t>(kWrowMaxWaves, (Nt + cus - 1) / cus);
+  g.rw = (int)std::min<int64_t>(kWrowMaxWaves, GEMV_WROW_RW > 0 ? GEMV_WROW_RW : (Nt + cus - 1) / cus);
   g.nb = (int)std::min<int64_t>(cus, (Nt + g.rw - 1) / g.rw);
   // the x staging covers K / 8 chunks with kWrowXIter per thread
   return (int64_t)g.rw * 64 * kWrowXIter * 8 >= K;
