@@ -34,7 +34,7 @@ python tools/pmc_traffic.py "$OUT/pmc" gemv_stream gemv_int4_g128_batched \
 (cd /tmp && step pmc_launches 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcl" \
    -o run -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode \
    --no-decode-layer --mode launches) || exit $?
-python tools/pmc_traffic.py "$OUT/pmcl" "gemv_fast_kernel<4, 1, 1, 0, 0, 2, false>" gemv_int4_g128 \
+python tools/pmc_traffic.py "$OUT/pmcl" "gemv_fast_kernel<4, 1, 1, 0, 0, 2, 0>" gemv_int4_g128 \
   "$OUT/${R}_gemv_int4_g128_pmc.json"
 # the sub-byte rings (configs[3]): FETCH_SIZE of the batched streaming launch
 for w in gemv_int3_g64 gemv_int2_g64; do
