@@ -299,13 +299,38 @@ def decode_layer_bench(args, dev, timed):
     return out
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """``--gpus N`` (N > 1) without a launcher: start N rank processes of this script through
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) as a CHILD process and return
+    its exit code.  Runs before anything in this process touches the GPU (no torch import here),
+    so no process that initialised HIP is replaced or forked."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     import torch
     import torch.distributed as dist
     from quant import qlin
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BENCH_DIST_BACKEND=gloo + BENCH_SHARE_GPU=1: rehearse the N > 1 path with several ranks on

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 11
+#define QLIN_ABI_VERSION 12
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -188,6 +188,15 @@ int64_t qlin_linear_workspace_bytes(int64_t M, int64_t N, int64_t K, int bits, i
  * arguments.  Introspection for tests and tools; no reference counterpart.
  */
 int qlin_gemm_block_cols(int64_t M, int64_t N, int bits);
+
+/*
+ * Which kernel a one-token-row product (qlin_gemv_f16 / qlin_linear_ep_f16 at M = 1, 16-B aligned
+ * x, and qlin_rmsnorm_linear_ep_f16) of this shape runs on the current device: 1 = the whole-row
+ * kernel (wide matrices), 2 = the fast split-K kernel, 3 = the rows kernel (long K), 0 = the
+ * general GEMV kernel (no M = 1 route: qlin_rmsnorm_linear_ep_f16 rejects the shape), -1 =
+ * invalid arguments.  Introspection for tests and tools (ABI 12); no reference counterpart.
+ */
+int qlin_gemv_m1_route(int64_t N, int64_t K, int bits, int group);
 
 /*
  * The packed linear with a fused output epilogue (the decoder layer's glue around two of its

@@ -1582,6 +1582,14 @@ extern "C" int qlin_rmsnorm_linear_supported(int64_t M, int64_t N, int64_t K, in
   return rmsnorm_linear_ok(M, N, K, bits, group) ? 1 : 0;
 }
 
+extern "C" int qlin_gemv_m1_route(int64_t N, int64_t K, int bits, int group) {
+  if (N < 1 || !valid_layout(N, K, bits, group)) return -1;
+  WrowGeo wg;
+  RowsGeo rg;
+  int W = 0, lw = 0, tpw = 0;
+  return m1_route(N, (int)K, group, nullptr, nullptr, wg, W, lw, tpw, rg);
+}
+
 extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                                           const uint16_t* x, const void* norm_weight, float eps,
                                           const uint16_t* bias, const uint16_t* residual,

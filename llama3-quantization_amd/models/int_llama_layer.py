@@ -299,8 +299,11 @@ class QuantLlamaAttention(nn.Module):
 
     # graph-replayed decode steps (models/pipeline.py generate(graphs=True)): an int32 device
     # tensor holding the step's cache length; the step then reads nothing on the host (no past /
-    # mask / length checks), appends to and attends over the kv_cache buffers in self._kv
+    # mask / length checks), appends to and attends over the kv_cache buffers in self._kv;
+    # _dyn_max: the longest length the captured steps reach (None: the buffers' capacity), which
+    # sizes the attention grid and must stay within qlin.ATTN_MAX_L
     _dyn_len = None
+    _dyn_max = None
 
     def _decode_step_len(self, hidden_states, position_ids, residual, prenorm):
         """One token through the fused packed attention with the cache length on the device
@@ -316,7 +319,8 @@ class QuantLlamaAttention(nn.Module):
         cos_c, sin_c = self._rope_cache(buf[0], buf[0].shape[2])
         attn = qlin.attn_decode_rope_len(q, k, v, cos_c, sin_c, position_ids, self.num_heads,
                                          self.num_key_value_heads, self.head_dim, buf[0], buf[1],
-                                         self._dyn_len, out_dtype=torch.float16)
+                                         self._dyn_len, out_dtype=torch.float16,
+                                         max_len=self._dyn_max)
         attn = attn.transpose(1, 2).reshape(bsz, 1, self.hidden_size)
         return self._out(attn, residual), None, None
 

@@ -175,21 +175,21 @@ class PipelineRunner:
                 bufs[j] = at._kv
         return h
 
-    def _layers_step_len(self, h, mb, pos, length):
+    def _layers_step_len(self, h, mb, pos, length, max_len):
         """This stage's layers over one token per sequence with the cache length on the device
-        (each layer's attention in its device-length mode over micro-batch ``mb``'s buffers):
-        the launch sequence of every decode step, captured once per micro-batch."""
-        n = len(self.model.layers)
+        (each layer's attention in its device-length mode over micro-batch ``mb``'s buffers, its
+        grid sized for ``max_len``, the longest length of the generation): the launch sequence of
+        every decode step, captured once per micro-batch."""
         bufs = self._bufs[mb]
         for j, layer in enumerate(self.model.layers):
             at = layer.self_attn
             at._kv = bufs[j]
-            at._dyn_len = length
+            at._dyn_len, at._dyn_max = length, max_len
             try:
                 h = layer(h, attention_mask=None, position_ids=pos, past_key_value=None,
                           use_cache=False)[0]
             finally:
-                at._dyn_len = None
+                at._dyn_len = at._dyn_max = None
         return h
 
     def _graph_step(self, h, mb, pos0, cap_rows, replay):
@@ -214,18 +214,20 @@ class PipelineRunner:
         st["pos"].fill_(pos0)
         st["len"].fill_(pos0 + 1)
         if not replay:
-            return self._layers_step_len(st["h"], mb, st["pos"], st["len"])
+            return self._layers_step_len(st["h"], mb, st["pos"], st["len"], cap_rows)
         if st["graph"] is None:
-            # one eager pass first (workspaces, rotary tables), then the capture; both rewrite
-            # the same cache row pos0 with the same values before the replay below
+            # one eager pass first (workspaces, rotary tables, the attention's merge counters,
+            # which are kept per stream), then the capture ON THE SAME STREAM, so nothing is first
+            # allocated inside the capture; both passes rewrite the same cache row pos0 with the
+            # same values before the replay below
             s_ = torch.cuda.Stream(h.device)
             s_.wait_stream(torch.cuda.current_stream(h.device))
             with torch.cuda.stream(s_):
-                self._layers_step_len(st["h"], mb, st["pos"], st["len"])
-            torch.cuda.current_stream(h.device).wait_stream(s_)
+                self._layers_step_len(st["h"], mb, st["pos"], st["len"], cap_rows)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                st["out"] = self._layers_step_len(st["h"], mb, st["pos"], st["len"])
+            with torch.cuda.graph(g, stream=s_):
+                st["out"] = self._layers_step_len(st["h"], mb, st["pos"], st["len"], cap_rows)
+            torch.cuda.current_stream(h.device).wait_stream(s_)
             st["graph"] = g
         st["graph"].replay()
         return st["out"].clone()
@@ -257,6 +259,11 @@ class PipelineRunner:
             meta = self._bcast(meta.to(self.device), 0).cpu()
         n_micro, B, T = (int(v) for v in meta.tolist())
         H = self.hidden_shape[-1]
+        from quant import qlin
+        if device_len and T + n_new > qlin.ATTN_MAX_L:
+            # the device-length attention serves at most ATTN_MAX_L cache rows: longer
+            # generations take the per-step path (whose attention leaves the kernel there)
+            device_len = graphs = False
         self._past, self._bufs, self._gstate = {}, {}, {}
         out = torch.zeros(n_micro, B, n_new, dtype=torch.int64, device=self.device)
         # next-token hand-back on a communicator of its own (first <-> last stage): each
@@ -271,6 +278,10 @@ class PipelineRunner:
         cur = [None] * n_micro  # next input tokens [B, 1] per micro-batch (first stage)
         tok_reqs, pending = [], []
         for step in range(n_new):
+            # stages run ahead (no per-step drain), but sends that have completed are released
+            # once per step, so held buffers stay bounded instead of growing with n_new * n_micro
+            pending = [p for p in pending if not p[0].is_completed()]
+            tok_reqs = [p for p in tok_reqs if not p[0].is_completed()]
             T_in, pos0 = (T, 0) if step == 0 else (1, T + step - 1)
             for i in range(n_micro):
                 if info.first:

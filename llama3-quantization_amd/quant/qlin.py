@@ -18,7 +18,7 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -52,6 +52,7 @@ SIGNATURES = {
                                _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_block_cols": ([_l, _l, _i], _i),
+    "qlin_gemv_m1_route": ([_l, _l, _i, _i], _i),
     "qlin_linear_workspace_bytes": ([_l, _l, _l, _i, _i, _i], _l),
     "qlin_linear_ep_f16": ([_p, _p, _i, _p, _p, _p, _p, _l, _l, _l, _i, _i, _i, _i, _i, _p, _l, _p],
                            _i),
@@ -413,6 +414,19 @@ def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NON
     return y
 
 
+M1_GENERAL, M1_WHOLE_ROW, M1_FAST, M1_ROWS = 0, 1, 2, 3
+
+
+def m1_route(N, K, bits, group):
+    """The kernel a one-token-row product of this shape runs (``qlin_gemv_m1_route``):
+    M1_WHOLE_ROW (wide matrices), M1_FAST (split-K fast kernel), M1_ROWS (long K) or M1_GENERAL
+    (the general GEMV kernel; no fused RMSNorm there)."""
+    r = load_library().qlin_gemv_m1_route(N, K, bits, group)
+    if r < 0:
+        raise ValueError(f"m1_route: invalid shape N={N} K={K} b{bits} g{group}")
+    return r
+
+
 def rmsnorm_linear_supported(M, N, K, bits, group):
     """Whether ``rmsnorm_linear_ep`` takes this shape (one token row on the fast GEMV path)."""
     return bool(load_library().qlin_rmsnorm_linear_supported(M, N, K, bits, group))
@@ -733,10 +747,16 @@ def attn_decode_rope(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_
 
 
 def attn_decode_rope_len(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n_kv_heads,
-                         head_dim, k_cache, v_cache, length, out_dtype=torch.float32):
+                         head_dim, k_cache, v_cache, length, out_dtype=torch.float32,
+                         max_len=None):
     """``qlin_attn_decode_rope_len``: attn_decode_rope for graph-replayed decode steps — the cache
-    length (this step's new row + 1) is read from the int32 device tensor ``length`` [1], the
-    grid is sized for the caches' capacity (k_cache.shape[2] rows); no mask."""
+    length (this step's new row + 1) is read from the int32 device tensor ``length`` [1]; no mask.
+
+    ``max_len``: the largest length ``length`` will hold over the captured steps (default: the
+    caches' capacity, k_cache.shape[2] rows); the grid and the partials are sized for it.  It
+    must fit the caches and the kernel's ATTN_MAX_L rows — a longer sequence has to take the
+    per-step path (the kernel clamps the device length to max_len, so a length beyond it would
+    attend over a prefix and rewrite row max_len - 1: rejected here, not clamped)."""
     for t_ in (q, k, v):
         if _rows(t_) is None:
             raise ValueError("attn_decode_rope_len takes row-strided [B, 1, H*D] q / k / v")
@@ -750,7 +770,10 @@ def attn_decode_rope_len(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n
     if not (k_cache.is_contiguous() and v_cache.is_contiguous()) or k_cache.shape != v_cache.shape \
             or tuple(k_cache.shape[:2]) != (B, n_kv_heads) or k_cache.shape[3] != head_dim:
         raise ValueError("attn_decode_rope_len takes contiguous [B, Hkv, rows, D] caches")
-    cap = min(k_cache.shape[2], ATTN_MAX_L)
+    cap = k_cache.shape[2] if max_len is None else int(max_len)
+    if cap < 1 or cap > k_cache.shape[2] or cap > ATTN_MAX_L:
+        raise ValueError(f"attn_decode_rope_len: max length {cap} must fit the cache "
+                         f"({k_cache.shape[2]} rows) and ATTN_MAX_L ({ATTN_MAX_L})")
     pos, pbs = _pos_ids(position_ids, B, 1)
     out = torch.empty(B, n_heads, 1, head_dim, dtype=out_dtype, device=q.device)
     lib = load_library()

@@ -147,6 +147,38 @@ def test_attn_decode_rope_len_matches(B, Hq, Hkv, kv0, cap):
         assert (got - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
 
 
+def test_attn_decode_rope_len_bounds():
+    """The device-length attention sizes its grid for ``max_len`` (the longest length the captured
+    steps will reach) and refuses caches / lengths past ATTN_MAX_L rows instead of clamping (a
+    clamped length would attend over a prefix and rewrite row ATTN_MAX_L - 1); with max_len the
+    grid of a large-capacity cache covers exactly the steps' lengths."""
+    from models.int_llama_layer import LlamaRotaryEmbedding437
+    B, Hq, Hkv, D = 1, 32, 8, 128
+    g = torch.Generator(device="cuda").manual_seed(3)
+    qkv = (torch.randn(B, 1, (Hq + 2 * Hkv) * D, device="cuda", generator=g) * 2).half()
+    q, k, v = torch.split(qkv, [Hq * D, Hkv * D, Hkv * D], dim=-1)
+    rot = LlamaRotaryEmbedding437(D, 8192, 500000.0, device="cuda").half()
+    cos, sin = rot.cos_cached.float().contiguous(), rot.sin_cached.float().contiguous()
+    big = qlin.ATTN_MAX_L + 256
+    kc = torch.randn(B, Hkv, big, D, device="cuda", generator=g).half()
+    vc = torch.randn(B, Hkv, big, D, device="cuda", generator=g).half()
+    kv0 = 700
+    pos = torch.full((B, 1), kv0, device="cuda", dtype=torch.int64)
+    length = torch.tensor([kv0 + 1], dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):  # capacity past ATTN_MAX_L and no max_len
+        qlin.attn_decode_rope_len(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, length)
+    with pytest.raises(ValueError):
+        qlin.attn_decode_rope_len(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, length,
+                                  max_len=qlin.ATTN_MAX_L + 1)
+    kc2, vc2 = kc.clone(), vc.clone()
+    got = qlin.attn_decode_rope_len(q, k, v, cos, sin, pos, Hq, Hkv, D, kc, vc, length,
+                                    max_len=kv0 + 1)
+    ref = qlin.attn_decode_rope(q, k, v, cos, sin, pos, Hq, Hkv, D, kc2, vc2, kv0, None,
+                                math.sqrt(D))
+    assert torch.equal(got, ref)  # max_len == length: the per-step launch's split, same bits
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+
+
 def test_attn_decode_rejects_unsupported():
     q = torch.randn(1, 32, 1, 64, device="cuda")
     k = torch.randn(1, 8, 10, 64, device="cuda").half()

@@ -1,0 +1,52 @@
+"""bench.py's multi-rank path (the driver's 1/2/4/8-GPU scaling runs): ``--gpus N`` without a
+launcher starts N rank processes itself, and the rank-0 JSON line reports the whole job.
+
+Rehearsed on one MI355X with two ranks sharing the card (BENCH_DIST_BACKEND=gloo,
+BENCH_SHARE_GPU=1: the barrier and the max-over-ranks reduction go through gloo; the driver's
+multi-GPU runs use RCCL, one rank per GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, extra_env=None, timeout=600):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(extra_env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]  # ONE JSON line, from rank 0
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("split", [False, True])
+def test_bench_gpus2_spawns_ranks(split):
+    """--gpus 2 (weak: an independent ring per rank; --split: output rows of one shared ring):
+    two ranks ran, n_gpus is 2 and value is the whole-job throughput."""
+    args = ["--gpus", "2", "--steps", "6", "--warmup", "2", "--ring", "16", "--ramp-s", "0.05",
+            "--no-cpu-baseline", "--no-decode-layer", "--no-other-mode"]
+    if split:
+        args.append("--split")
+    d = _bench(*args, extra_env={"BENCH_DIST_BACKEND": "gloo", "BENCH_SHARE_GPU": "1"})
+    assert d["n_gpus"] == 2
+    assert d["scaling"] == ("strong" if split else "weak")
+    assert d["config"]["ring"] == 16 and d["steps"] == 6
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    # value = all ranks' products / the max-over-ranks time
+    per_rank_products = 16 * 6
+    flops = 2.0 * 4096 * 4096 * per_rank_products * (1 if split else 2)
+    if split:  # N_per_rank rows each: the job is the one shared ring
+        assert d["config"]["N_per_rank"] == 2048
+    got = flops / (d["ms_per_step"] * 6 / 1e3) / 1e12
+    assert abs(got - d["value"]) <= 0.02 * d["value"] + 1e-3, (got, d["value"])

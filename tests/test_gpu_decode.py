@@ -27,12 +27,15 @@ linear output) with only the summation order of F.linear changed:
   fake_quant_ksplit   the same in two K halves added in fp32 (another association);
   fake_quant_f64acc   the sum accumulated in float64 (the exactly rounded order).
 The order floor is the largest distance of a twin to the fake-quant logits (each twin's own
-distance is reported beside it).  The bar on every seed: each packed / fused
-path's max and p99 distance to the fake-quant logits <= 1.1 x the floor's, and its error against
-float64 <= 1.1 x the largest float64 error among the reference and its twins (the reference
-arithmetic's own spread: on seed 21 the F.linear-order twin alone is 1.12 x the reference).
-Numbers are written to $QLIN_PARITY_OUT (profiles/r4_decode_parity.json, r4_prefill_parity.json,
-r4_prefill32_parity.json)."""
+distance is reported beside it, and every path's ratio to the single hipBLASLt twin
+``fake_quant_f32lin`` too).
+
+The bar (declared before these runs), over >= 8 seeds per
+4-layer case (4 seeds for the 32-layer window), for every packed / fused path:
+  * ratio of its max logit distance to the max-of-twins floor: median <= 1.0, max <= 1.1;
+  * ratio of its float64 error to the reference's own float64 error: median <= 1.05.
+The p99 ratios are reported beside them.  Numbers are written to $QLIN_PARITY_OUT*
+(profiles/r5_decode_parity.json, r5_prefill_parity.json, r5_prefill32_parity.json)."""
 import json
 import math
 import os
@@ -51,8 +54,11 @@ from quant.utils import pack_quant_linears  # noqa: E402
 
 LAYERS = 4
 KV = 512
-SEEDS = (21, 31, 41)
-BAR = 1.1
+SEEDS = (21, 31, 41, 51, 61, 71, 81, 91)
+SEEDS32 = (21, 31, 41, 51)
+BAR_MAX = 1.1         # max over seeds of the max-distance ratio to the max-of-twins floor
+BAR_MEDIAN = 1.0      # median over seeds of that ratio
+BAR_FP64_MEDIAN = 1.05  # median over seeds of (float64 error / the reference's own)
 
 
 def _cfg(layers=LAYERS):
@@ -193,38 +199,53 @@ def _report(seed, paths, model, cfg, ref64_h):
 
 
 def _judge(reps, ref_name="fake_quant", out_env=None):
-    """Per seed: every other path within BAR x the order floor (the twins' largest distance to
-    the fake-quant logits, max and p99 separately) and BAR x the reference's own float64 error."""
-    failures = []
+    """Per path, over the seeds: the ratio of its max (and p99) logit distance to the fake-quant
+    logits against the max-of-twins order floor and against the single hipBLASLt twin, and of
+    its float64 error against the reference's own; the bar (module docstring) on the median and
+    max of those ratios."""
+    import statistics
+    ratios = {}
     for rep in reps:
         fq = rep[ref_name]
         fmax = max(rep[t]["logits_max_vs_fake_quant"] for t in TWINS)
         fp99 = max(rep[t]["logits_p99_vs_fake_quant"] for t in TWINS)
-        # the float64 bar, like the distance bar, is the reference arithmetic's own spread: the
-        # largest float64 error among the reference and its reorder twins
-        f64 = max([fq["logits_err_vs_fp64"]] + [rep[t]["logits_err_vs_fp64"] for t in TWINS])
-        crit = {"max_vs_fake_quant": BAR * fmax, "p99_vs_fake_quant": BAR * fp99,
-                "err_vs_fp64": BAR * f64, "order_floor_fp64": f64,
-                "order_floor_max": fmax, "order_floor_p99": fp99,
-                "order_floor_twins_max": {t: rep[t]["logits_max_vs_fake_quant"] for t in TWINS}}
-        rep["criteria"] = crit
+        rep["criteria"] = {"order_floor_max": fmax, "order_floor_p99": fp99,
+                           "reference_fp64_err": fq["logits_err_vs_fp64"],
+                           "order_floor_twins_max": {t: rep[t]["logits_max_vs_fake_quant"]
+                                                     for t in TWINS}}
         for name, r in rep.items():
             if name in (ref_name, "criteria", "seed") or name in TWINS or not isinstance(r, dict):
                 continue
-            r["ratio_max_to_floor"] = r["logits_max_vs_fake_quant"] / crit["order_floor_max"]
-            r["ratio_p99_to_floor"] = r["logits_p99_vs_fake_quant"] / crit["order_floor_p99"]
-            if r["logits_max_vs_fake_quant"] > crit["max_vs_fake_quant"]:
-                failures.append((rep["seed"], name, "max", r["logits_max_vs_fake_quant"]))
-            if r["logits_p99_vs_fake_quant"] > crit["p99_vs_fake_quant"]:
-                failures.append((rep["seed"], name, "p99", r["logits_p99_vs_fake_quant"]))
-            if r["logits_err_vs_fp64"] > crit["err_vs_fp64"]:
-                failures.append((rep["seed"], name, "fp64", r["logits_err_vs_fp64"]))
-    doc = {"bar": f"<= {BAR} x order floor per seed", "seeds": reps, "failures": failures}
+            r["ratio_max_to_floor"] = r["logits_max_vs_fake_quant"] / fmax
+            r["ratio_p99_to_floor"] = r["logits_p99_vs_fake_quant"] / fp99
+            r["ratio_max_to_f32lin_twin"] = (r["logits_max_vs_fake_quant"] /
+                                             rep["fake_quant_f32lin"]["logits_max_vs_fake_quant"])
+            r["ratio_fp64_to_reference"] = r["logits_err_vs_fp64"] / fq["logits_err_vs_fp64"]
+            ratios.setdefault(name, []).append(r)
+    summary, failures = {}, []
+    for name, rs_ in ratios.items():
+        col = lambda k: [r[k] for r in rs_]  # noqa: E731
+        sm = {k: {"median": statistics.median(col(k)), "max": max(col(k)), "min": min(col(k))}
+              for k in ("ratio_max_to_floor", "ratio_p99_to_floor", "ratio_max_to_f32lin_twin",
+                        "ratio_fp64_to_reference")}
+        sm["top1_min"] = min(col("logits_top1_vs_fake_quant"))
+        summary[name] = sm
+        if sm["ratio_max_to_floor"]["median"] > BAR_MEDIAN:
+            failures.append((name, "median ratio_max_to_floor", sm["ratio_max_to_floor"]["median"]))
+        if sm["ratio_max_to_floor"]["max"] > BAR_MAX:
+            failures.append((name, "max ratio_max_to_floor", sm["ratio_max_to_floor"]["max"]))
+        if sm["ratio_fp64_to_reference"]["median"] > BAR_FP64_MEDIAN:
+            failures.append((name, "median ratio_fp64_to_reference",
+                             sm["ratio_fp64_to_reference"]["median"]))
+    doc = {"bar": {"ratio_max_to_floor": f"median <= {BAR_MEDIAN}, max <= {BAR_MAX}",
+                   "ratio_fp64_to_reference": f"median <= {BAR_FP64_MEDIAN}",
+                   "declared": "before the runs (VERDICT r4 item 2; DESIGN.md §2)"},
+           "n_seeds": len(reps), "summary": summary, "failures": failures, "seeds": reps}
     out = os.environ.get(out_env or "QLIN_PARITY_OUT")
     if out:
         with open(out, "w") as f:
             json.dump(doc, f, indent=1)
-    print(json.dumps(doc))
+    print(json.dumps({"summary": summary, "failures": failures}))
     for rep in reps:
         assert rep[ref_name]["logits_err_vs_fp64"] < 1e-2, rep
     assert not failures, failures
@@ -260,6 +281,23 @@ def _decode_seed(seed):
                       use_cache=kv_cache)[0]
         return h[0, 0]
 
+    def run_dyn_len():
+        """The device-length launches generate(graphs=True) captures and replays: the cache
+        length read from a device tensor, the attention grid sized for a generation 64 tokens
+        longer, no host-side mask / past (models/pipeline.py _layers_step_len)."""
+        h = x
+        length = torch.tensor([KV + 1], dtype=torch.int32, device=dev)
+        for i, layer in enumerate(model.layers):
+            at = layer.self_attn
+            at.adopt_kv_cache(past[i], rows=KV + 65)
+            at._dyn_len, at._dyn_max = length, KV + 65
+            try:
+                h = layer(h, attention_mask=None, position_ids=pos, past_key_value=None,
+                          use_cache=False)[0]
+            finally:
+                at._dyn_len = at._dyn_max = None
+        return h[0, 0]
+
     paths = {"fake_quant": run()}
     for name, fn in TWINS.items():
         _reorder_reference(model, fn)
@@ -271,6 +309,7 @@ def _decode_seed(seed):
     for layer in model.layers:
         layer.fuse_packed_projections(kv_cache=True)
     paths["fused_kv_cache"] = run(kv_cache=True)
+    paths["fused_device_len"] = run_dyn_len()
     _progress("decode seed", seed, "paths done")
     rep = _report(seed, paths, model, cfg, h64)
     rep.update(layers=LAYERS, kv_len=KV + 1,
@@ -333,7 +372,7 @@ def _prefill_seed(seed, layers, S):
 @torch.no_grad()
 def test_full_width_prefill_three_way():
     """A 256-token causal window (positions 0..255) through four full-width layers: fake-quant,
-    its reordered twin, packed (MFMA GEMM), the fused layer, and the fused layer + the fused
+    its reordered twins, packed (MFMA GEMM), the fused layer, and the fused layer + the fused
     prefill-attention kernel (opt-in mode, DESIGN.md §4 qlin_attn_prefill)."""
     _judge([_prefill_seed(s, LAYERS, 256) for s in SEEDS], out_env="QLIN_PARITY_OUT_PREFILL")
 
@@ -343,4 +382,4 @@ def test_full_depth_prefill_attention_mode():
     """The opt-in prefill-attention mode through all 32 LLaMA3-8B layers (a 128-token window):
     amplified over 32 random layers, its distance to the fake-quant logits is held to the
     reference's own order floor at the same depth."""
-    _judge([_prefill_seed(s, 32, 128) for s in SEEDS[:2]], out_env="QLIN_PARITY_OUT_PREFILL32")
+    _judge([_prefill_seed(s, 32, 128) for s in SEEDS32], out_env="QLIN_PARITY_OUT_PREFILL32")

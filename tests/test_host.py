@@ -71,6 +71,11 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert lib.qlin_rmsnorm_linear_supported(1, 16, 1000, 4, 40) == 0
     assert lib.qlin_rmsnorm_linear_ep_f16(p, p, 0, p, p, 1e-5, None, None, p, 1, 16, 256, 4, 128,
                                           1, None) == 1  # residual epilogue without residual
+    # ABI 12: which M = 1 kernel a shape takes (without a device: the 256-CU MI355X geometry)
+    assert lib.qlin_gemv_m1_route(28672, 4096, 4, 128) == 1   # gate/up: whole-row kernel
+    assert lib.qlin_gemv_m1_route(6144, 4096, 3, 64) == 2     # q/k/v: fast kernel
+    assert lib.qlin_gemv_m1_route(4096, 14336, 2, 32) == 3    # down: rows kernel
+    assert lib.qlin_gemv_m1_route(4096, 1000, 4, 40) == -1    # invalid layout
     assert lib.qlin_pack_codes(None, 16, 64, 4, None, None) == 1
     assert lib.qlin_pack_codes(p, 16, 48, 4, p, None) == 1  # K % 32
     assert lib.qlin_pack_codes(p, 16, 64, 5, p, None) == 1  # bits
