@@ -43,7 +43,10 @@ def _case(N, K, bits, group, zmode, seed):
     G = K // group
     dev = "cuda"
     u = torch.randint(0, 2 ** bits, (N, K), generator=g, device=dev, dtype=torch.int32)
-    s = (torch.rand(N, G, generator=g, device=dev) * 4e-3 + 5e-4).half()
+    # wide zeros (|u - z| up to ~1e4) get 100x smaller scales, so outputs and the SiLU * up
+    # products stay inside the fp16 range
+    s = ((torch.rand(N, G, generator=g, device=dev) * 4e-3 + 5e-4) *
+         (1e-2 if zmode == "wide" else 1.0)).half()
     flags = 0
     if zmode == "float":
         z = (torch.rand(N, G, generator=g, device=dev) * (2 ** bits - 1)).half()
@@ -74,6 +77,18 @@ def _rmsnorm_ref(x, w16):
     return (w16.astype(np.float32) * (x32 * r)).astype(np.float16)
 
 
+def _assert_residual(y, lin64, res, what):
+    """RN16(res + RN16(linear)) (the reference's fp16 ``residual + o_proj(x)``) against float64:
+    the GEMV tolerance on the linear part plus the two fp16 roundings (half an ulp of the linear
+    output and of the sum), which dominate where res and the linear output nearly cancel."""
+    y = y.astype(np.float64)
+    ref = res.astype(np.float64) + lin64
+    bound = (2e-3 * (np.abs(lin64) + np.abs(lin64).max() / 16.0) +
+             2.0 ** -11 * (np.abs(lin64) + np.abs(ref)) + 1e-6)
+    bad = np.abs(y - ref) > bound
+    assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} outside tolerance"
+
+
 def _silu_mul64(y64):
     """Rows interleaved in 8-row halves per 16-row tile (gate rows, then up rows)."""
     v = y64.reshape(y64.shape[0], -1, 2, 8)
@@ -99,7 +114,7 @@ def _check_routes(name, bits, group, zmode):
     assert_close_to_ref(y.view(1, N).cpu().numpy(), ref[:1] + bias, what=what + " +bias")
     y = qlin.linear_ep(xs, qw, qsz, None, N, K, bits, group, fl, epilogue=qlin.EP_RESIDUAL,
                        residual=t(res).view(1, 1, N))
-    assert_close_to_ref(y.view(1, N).cpu().numpy(), ref[:1] + res, what=what + " residual")
+    _assert_residual(y.view(1, N).cpu().numpy(), ref[:1], res, what=what + " residual")
     nw = t(w16)
     y = qlin.rmsnorm_linear_ep(xs, nw, EPS, qw, qsz, None, N, K, bits, group, fl)
     assert_close_to_ref(y.view(1, N).cpu().numpy(), ref[1:], what=what + " rmsnorm")

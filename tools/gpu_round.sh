@@ -13,8 +13,9 @@ STEPS="${STEPS:-tests smoke bench prof}"
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
-      rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"; ok_or_stop $rc pytest ;;
+      timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} -m gpu -v --maxfail=20 -p no:cacheprovider \
+        --timeout ${TEST_CASE_TIMEOUT:-300} --timeout-method thread > "$OUT/pytest_gpu${TAG:-}.log" 2>&1
+      rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu${TAG:-}.log"; ok_or_stop $rc pytest ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       rc=$?; echo "smoke rc=$rc"; tail -2 "$OUT/smoke.log"; ok_or_stop $rc smoke ;;
