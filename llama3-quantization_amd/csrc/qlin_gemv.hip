@@ -632,21 +632,27 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Decode path for wide matrices (one token row, N >= 16 tile rows per CU): the "whole-row" kernel.
+// Decode path for wide matrices (one token row, >= 4 tile rows per CU): the work-queue kernel.
 //
-// The rows kernel splits every tile row's K over the W waves of a block, so each row ends in a
-// block barrier; over many rows those barriers lock the waves together and a row costs the
-// slowest wave's latency.  For wide matrices (gate/up: 1,792 tile rows) there are enough rows to
-// give every wave whole rows instead, as the batched streaming kernel does: wave w streams all K
-// of its tile row(s) with PF tiles in flight, one MFMA chain per row in k order (bit-identical
-// to qlin_gemm_f16 without split-K), and applies the epilogue itself (the gate / up halves of an
-// interleaved row tile meet by a lane shuffle).  The block's waves share x: it is staged once per
-// block in LDS (16-B chunks read by all threads; with the RMSNorm, normalised there at the
+// One 8-wave block per CU owns the tile rows b, b + nb, b + 2 nb, ... (gate/up: 1,792 rows, 7 per
+// CU).  Their tiles form chunks of kWqC = 4 consecutive k-tiles of one row; the waves take chunks
+// from a counter in LDS (the first kWqD each statically), keep kWqD chunks of loads in flight
+// (codes nt-loaded to registers, the chunk's (scale, zero) words with ONE load per chunk), and
+// store each chunk's 16 partial sums in LDS; after one block barrier every row's chunks are added
+// in k order (deterministic: the same order whatever wave ran which chunk) and the epilogue is
+// applied.  Why a queue: with whole rows per wave (round 4's kernel) the second wave of each SIMD
+// finished ~3 us after the first — the CU serves its waves' requests oldest first, so statically
+// equal shares end unequally; waves that are served sooner now simply take more chunks
+// (tools/dev/wq_lab.hip: gate/up + norm + SiLU 17.0 -> 14.3-15.3 us per launch, one box).
+//
+// x is staged once per block in LDS (16-B chunks; with the RMSNorm normalised there at the
 // reference's rounding point after one block reduction of the sum of squares), and every A
-// fragment is a broadcast ds_read_b128 of it.  No barrier after the staging.
+// fragment is a broadcast ds_read_b128 of it.  A chunk's (scale, zero) words go through a per-wave
+// LDS slot (one ds_write, then one ds_read_b32 per tile and group slot).
 // ---------------------------------------------------------------------------------------------
-constexpr int kWrowMaxWaves = 8;
-constexpr int kWrowXIter = 4;  // 16-B x chunks per thread (host: K <= 8 * 64 * waves * kWrowXIter)
+constexpr int kWqWaves = 8;  // waves per block (one block per CU)
+constexpr int kWqC = 4;      // k-tiles per chunk
+constexpr int kWqD = 2;      // chunks in flight per wave
 
 struct WrowArgs {
   const uint32_t* qw;
@@ -660,35 +666,48 @@ struct WrowArgs {
   int ep, has_bias;     // bias / res always readable (the host points absent ones at y)
   int64_t nres;         // readable elements at res
   int N, K, Kt, G, Nt;
-  int nwaves;           // waves of the grid: wave g owns tile rows g, g + nwaves, ...
+  int nb, CPR;          // blocks (block b: rows b, b + nb, ...); chunks per row (Kt / kWqC)
+  int part_off, sz_off, misc_off;  // LDS byte offsets (x staging at 0)
   uint32_t cmagic;
-#ifdef GEMV_ROWS_STAMP  // dev build only: per-wave stamps, as the rows kernel's
-  uint64_t* stamps;
-#endif
 };
 
-template <int BITS, int GPT, int ZM, int PF, int NRM>
-__global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const WrowArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xs4[];  // x (normed), fp16 [K]: K / 8 chunks
-  __shared__ float nss[kWrowMaxWaves];
+// LDS bytes of a launch: x (fp16 [K]) | partials [rows x CPR][16] fp32 | (scale, zero) slots
+// [waves][kWqD][64 GPT] words | the wave sums of squares [8] and the chunk counter
+inline void wq_lds_layout(int K, int max_rows, int CPR, int GPT, int& part_off, int& sz_off,
+                          int& misc_off, int& total) {
+  part_off = (K * 2 + 15) / 16 * 16;
+  sz_off = part_off + max_rows * CPR * kTileN * 4;
+  misc_off = sz_off + kWqWaves * kWqD * 64 * GPT * 4;
+  total = misc_off + (kWqWaves + 4) * 4;
+}
+
+template <int BITS, int GPT, int ZM, int NRM, int XI>
+__global__ __launch_bounds__(64 * kWqWaves) void gemv_wq_kernel(const WrowArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // ONE LDS object
+  uint4* xs4 = reinterpret_cast<uint4*>(lds);
+  float* part = reinterpret_cast<float*>(lds + a.part_off);
+  uint32_t* szs = reinterpret_cast<uint32_t*>(lds + a.sz_off);
+  float* nss = reinterpret_cast<float*>(lds + a.misc_off);
+  int* ctr = reinterpret_cast<int*>(lds + a.misc_off) + kWqWaves;
+  constexpr int nthr = 64 * kWqWaves, C = kWqC, D = kWqD;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15, q = lane >> 4;
-  const int nthr = blockDim.x;
-  const int gw = blockIdx.x * (nthr >> 6) + wave;  // this wave's grid index
-  const int nrow = gw < a.Nt ? (a.Nt - 1 - gw) / a.nwaves + 1 : 0;  // rows of this wave
-  ROWS_STAMP(0);
+  const int b = blockIdx.x;
+  const int nrows = b < a.Nt ? (a.Nt - 1 - b) / a.nb + 1 : 0;
+  const int CPR = a.CPR;
+  const int NC = nrows * CPR;  // chunks of this block
   auto group_of_tile = [&](int kt) {
     return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
   };
 
-  // x chunks of this thread (clamped: repeats are never stored), issued first
+  // x chunks of this thread (clamped: repeats are never stored) and their norm weights, issued
+  // first
   const int nch = a.K >> 3;
-  uint4 xc[kWrowXIter];
-  // the chunk's 8 norm weights: two float4 (fp32) or one uint4 of fp16 (kNwF16: nc[2i + 1] unused)
-  float4 nc[NRM ? 2 * kWrowXIter : 1];
+  uint4 xc[XI];
+  float4 nc[NRM ? 2 * XI : 1];  // two float4 (fp32 weights) or one uint4 of fp16 (kNwF16)
 #pragma unroll
-  for (int i = 0; i < kWrowXIter; ++i) {
+  for (int i = 0; i < XI; ++i) {
     const int c = min(tid + i * nthr, nch - 1);
     xc[i] = reinterpret_cast<const uint4*>(a.x)[c];
     if constexpr (NRM == kNwF16) {
@@ -698,165 +717,173 @@ __global__ __launch_bounds__(64 * kWrowMaxWaves) void gemv_wrow_kernel(const Wro
       nc[2 * i + 1] = reinterpret_cast<const float4*>(a.nw)[2 * c + 1];
     }
   }
-
-  asm volatile("" ::: "memory");  // the x and norm-weight requests go out before the tiles'
-
-  // the first PF tiles of the wave's first row (rows of PF-tile rounds: Kt % PF == 0)
-  WTile<BITS, GPT> wt[PF];
-  const int64_t wrow = (int64_t)a.Kt * (64 * BITS), srow = (int64_t)a.G * kTileN;
-  // load cursor: row, k-tile (a wave without rows reads row Nt - 1's first round, never used:
-  // the first round's loads stay unconditional, so the x staging below waits for the x words
-  // alone — behind a wave-uniform branch the join made hipcc wait for every tile, vmcnt(0))
-  int64_t lr = min<int64_t>(gw, a.Nt - 1);
-  int lkt = 0;
-  const uint32_t* lqw = a.qw + lr * wrow + lane * BITS;
-  const uint32_t* lsz = a.qsz + lr * srow + n_in;
-  auto load = [&](int u) {
-    const int kt = lkt + u;
-    wt[u].pc = load_piece_nt<BITS>(lqw + kt * (64 * BITS));
-    const int g0 = group_of_tile(kt);
-#pragma unroll
-    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = lsz[(g0 + s) * kTileN];
+  // the epilogue operands of this thread's first output (output o = tid: row o / 16, column
+  // o % 16; SiLU: o / 8, o % 8), loaded unconditionally ahead of the weights
+  const int NO = a.ep == kEpSiluMul ? 8 : kTileN;  // outputs per row
+  auto out_row = [&](int o) { return (int64_t)b + (int64_t)(o / NO) * a.nb; };
+  const int64_t nbias = a.has_bias ? (int64_t)a.N : a.nres;  // readable bias elements
+  _Float16 ob0, ob1, ores;
+  auto load_epi = [&](int o) {
+    const int64_t row = min(out_row(o), (int64_t)a.Nt - 1) * kTileN + o % NO;
+    ob0 = a.bias[min(row, nbias - 1)];
+    ob1 = a.bias[min(row + 8, nbias - 1)];
+    ores = a.res[min(row, a.nres - 1)];
   };
+  load_epi(tid);
+  asm volatile("" ::: "memory");  // the x / norm-weight / epilogue requests go out first
+
+  // chunk loads: (scale, zero) words first (GPT per lane: lane l holds words GPT l .. GPT l + GPT
+  // - 1 of the chunk's 64 GPT), then the C tiles' codes; a chunk past the block's last (a wave's
+  // final prefetches) reads the block's first chunk again (L2-hot, never used)
+  const int64_t wrow = (int64_t)a.Kt * (64 * BITS), srow = (int64_t)a.G * kTileN;
+  Piece<BITS> wt[D][C];
+  uint32_t szc[D][GPT];
+  int gb[D];  // GPT == 1: the chunk's first group
+  auto load_chunk = [&](auto SET_, int c) {
+    constexpr int d = decltype(SET_)::value;
+    if (c >= NC) c = 0;
+    const int j = c / CPR, kt0 = (c - j * CPR) * C;
+    const int64_t r = (int64_t)b + (int64_t)j * a.nb;
+    const uint32_t* sp = a.qsz + r * srow;
+    if constexpr (GPT == 1) {
+      gb[d] = group_of_tile(kt0);
+      szc[d][0] = sp[min(gb[d] + (lane >> 4), a.G - 1) * kTileN + n_in];
+    } else if constexpr (GPT == 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(sp + (int64_t)kt0 * GPT * kTileN + 2 * lane);
+      szc[d][0] = v.x;
+      szc[d][1] = v.y;
+    } else {
+      const uint4 v = *reinterpret_cast<const uint4*>(sp + (int64_t)kt0 * GPT * kTileN + 4 * lane);
+      szc[d][0] = v.x;
+      szc[d][1] = v.y;
+      szc[d][2] = v.z;
+      szc[d][3] = v.w;
+    }
+    const uint32_t* qp = a.qw + r * wrow + (int64_t)kt0 * (64 * BITS) + lane * BITS;
 #pragma unroll
-  for (int u = 0; u < PF; ++u) load(u);
-  // the x words count as produced here: their use (the statistics) is scheduled after every
-  // tile request above has been issued
-#pragma unroll
-  for (int i = 0; i < kWrowXIter; ++i) {
-    asm volatile("" : "+v"(xc[i].x), "+v"(xc[i].y), "+v"(xc[i].z), "+v"(xc[i].w)::"memory");
-    if constexpr (NRM == kNwF16)
-      asm volatile("" : "+v"(nc[2 * i].x), "+v"(nc[2 * i].y), "+v"(nc[2 * i].z),
-                   "+v"(nc[2 * i].w)::"memory");
-    else if constexpr (NRM)
-      asm volatile("" : "+v"(nc[2 * i].x), "+v"(nc[2 * i].y), "+v"(nc[2 * i].z),
-                   "+v"(nc[2 * i].w), "+v"(nc[2 * i + 1].x), "+v"(nc[2 * i + 1].y),
-                   "+v"(nc[2 * i + 1].z), "+v"(nc[2 * i + 1].w)::"memory");
-  }
-  ROWS_STAMP(1);
+    for (int u = 0; u < C; ++u) wt[d][u] = load_piece_nt<BITS>(qp + u * (64 * BITS));
+  };
+  load_chunk(std::integral_constant<int, 0>{}, wave);
+  load_chunk(std::integral_constant<int, 1>{}, wave + kWqWaves);
+  if (tid == 0) *ctr = D * kWqWaves;
 
   // stage x (normed) in LDS: one block reduction for the statistics, one barrier
   if constexpr (NRM) {
 #pragma clang fp contract(off)
     float ss = 0.f;
 #pragma unroll
-    for (int i = 0; i < kWrowXIter; ++i) {
+    for (int i = 0; i < XI; ++i) {
       const h8 v = __builtin_bit_cast(h8, xc[i]);
       float s8 = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s8 = s8 + (float)v[j] * (float)v[j];
+      for (int e = 0; e < 8; ++e) s8 = s8 + (float)v[e] * (float)v[e];
       ss = ss + (tid + i * nthr < nch ? s8 : 0.f);
     }
     ss = wave_sum(ss);
     if (lane == 0) nss[wave] = ss;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     float tot = 0.f;
-    for (int w = 0; w < (nthr >> 6); ++w) tot += nss[w];
+#pragma unroll
+    for (int w = 0; w < kWqWaves; ++w) tot += nss[w];
     const float rn = rsqrtf(tot / (float)a.K + a.eps);
 #pragma unroll
-    for (int i = 0; i < kWrowXIter; ++i) {
+    for (int i = 0; i < XI; ++i) {
       const h8 v = __builtin_bit_cast(h8, xc[i]);
       float w8[8];
       if constexpr (NRM == kNwF16) {
         const h8 h = __builtin_bit_cast(h8, nc[2 * i]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w8[j] = (float)h[j];
+        for (int e = 0; e < 8; ++e) w8[e] = (float)h[e];
       } else {
         const float t8[8] = {nc[2 * i].x, nc[2 * i].y, nc[2 * i].z, nc[2 * i].w,
                              nc[2 * i + 1].x, nc[2 * i + 1].y, nc[2 * i + 1].z, nc[2 * i + 1].w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w8[j] = t8[j];
+        for (int e = 0; e < 8; ++e) w8[e] = t8[e];
       }
       h8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (_Float16)(w8[j] * ((float)v[j] * rn));
+      for (int e = 0; e < 8; ++e) o[e] = (_Float16)(w8[e] * ((float)v[e] * rn));
       xc[i] = __builtin_bit_cast(uint4, o);
     }
   }
 #pragma unroll
-  for (int i = 0; i < kWrowXIter; ++i)
+  for (int i = 0; i < XI; ++i)
     if (tid + i * nthr < nch) xs4[tid + i * nthr] = xc[i];
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  ROWS_STAMP(2);
-  if (nrow == 0) return;  // wave-uniform; no barrier below
 
   const Magics mg = make_magics<BITS>();
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  int64_t cr = gw;  // compute cursor: row, k-tile
-  int ckt = 0;
-  const int NO = a.ep == kEpSiluMul ? 8 : kTileN;
-  _Float16 ob0 = 0, ob1 = 0, ores = 0;
-  auto load_epi = [&](int64_t r) {  // the row's epilogue operands, early in its stream
-    // unconditional (absent operands point at y, never used): no wait at a branch join
-    const int64_t row = r * kTileN + min(n_in, NO - 1);
-    const int64_t nb_ = a.has_bias ? (int64_t)a.N : a.nres;  // readable bias elements
-    ob0 = a.bias[min(row, nb_ - 1)];
-    ob1 = a.bias[min(row + 8, nb_ - 1)];
-    ores = a.res[min(row, a.nres - 1)];
-  };
-  load_epi(cr);
-  auto compute = [&](int u) {
-    const int kt = ckt + u;
-    h8 xa[4];
+  uint32_t* wsz = szs + wave * (D * 64 * GPT);  // this wave's (scale, zero) slots
+  int cs[D] = {wave, wave + kWqWaves};
+  // compute the chunk in set d, prefetching the next chunk from the queue into the same set
+  auto run = [&](auto SET_) {
+    constexpr int d = decltype(SET_)::value;
+    const int c = cs[d];
+    if (c >= NC) return false;  // wave-uniform
+    int cn = 0;
+    if (lane == 0)
+      cn = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    cn = __builtin_amdgcn_readfirstlane(cn);
+    const int j = c / CPR, kc = c - j * CPR;
+    const int g0 = GPT == 1 ? gb[d] : 0;
+    uint32_t* slot = wsz + d * (64 * GPT);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, xs4[kt * 16 + 4 * s + q]);
-    auto step = [&](auto S_) {
-      constexpr int S = decltype(S_)::value;
-      uint32_t v[4];
-      const GroupQ gq = make_group_w<BITS, ZM>(wt[u].sz[S * GPT / 4]);
-      dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
-      const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
+    for (int i = 0; i < GPT; ++i) slot[GPT * lane + i] = szc[d][i];
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < C; ++u) {
+      const int kt = kc * C + u;
+      h8 xa[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xa[s] = __builtin_bit_cast(h8, xs4[kt * 16 + 4 * s + q]);
+      uint32_t sw[GPT];
+#pragma unroll
+      for (int i = 0; i < GPT; ++i)
+        sw[i] = GPT == 1 ? slot[(group_of_tile(kt) - g0) * kTileN + n_in]
+                         : slot[(GPT * u + i) * kTileN + n_in];
+      auto step = [&](auto S_) {
+        constexpr int S = decltype(S_)::value;
+        uint32_t v[4];
+        const GroupQ gq = make_group_w<BITS, ZM>(sw[S * GPT / 4]);
+        dequant_step<BITS, ZM, S>(wt[d][u], mg, gq, v);
+        const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
+      };
+      step(std::integral_constant<int, 0>{});
+      step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{});
+      step(std::integral_constant<int, 3>{});
+    }
+    load_chunk(SET_, cn);  // the set's registers are free again
+    cs[d] = cn;
+    if (lane < kTileN) part[(j * CPR + kc) * kTileN + lane] = acc[0];  // C row 0, column lane
+    return true;
+  };
+  for (;;) {
+    if (!run(std::integral_constant<int, 0>{})) break;
+    if (!run(std::integral_constant<int, 1>{})) break;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // every row: its chunks' partials in k order, then F.linear's fp16 output and the epilogue
+  for (int o = tid; o < nrows * NO; o += nthr) {
+    if (o != tid) load_epi(o);
+    const int64_t r = out_row(o);
+    const int n = o % NO;
+    auto total = [&](int nn, _Float16 bv) {
+      const float* p = part + (int64_t)(o / NO) * CPR * kTileN + nn;
+      float t = 0.f;
+      for (int kc = 0; kc < CPR; ++kc) t += p[kc * kTileN];
+      if (a.has_bias) t += (float)bv;
+      return (float)(_Float16)t;
     };
-    step(std::integral_constant<int, 0>{});
-    step(std::integral_constant<int, 1>{});
-    step(std::integral_constant<int, 2>{});
-    step(std::integral_constant<int, 3>{});
-  };
-  auto store = [&]() {  // C row 0 = acc[0] of lanes 0..15 (column n = lane)
-    float t = acc[0];
-    if (a.has_bias) t += (float)ob0;
-    t = (float)(_Float16)t;  // F.linear's fp16 output
-    const float up = __shfl(t, lane + 8);  // interleaved gate / up halves: lane n + 8 = up row n
     if (a.ep == kEpSiluMul) {
-      if (lane < 8 && cr * kTileN + lane + 8 < a.N)
-        a.y[cr * 8 + lane] = (_Float16)(silu_rn16(t) * up);
-    } else if (lane < kTileN && cr * kTileN + lane < a.N) {
+      if (r * kTileN + n + 8 < a.N) a.y[r * 8 + n] = (_Float16)(silu_rn16(total(n, ob0)) * total(n + 8, ob1));
+    } else if (r * kTileN + n < a.N) {
+      float t = total(n, ob0);
       if (a.ep == kEpResidual) t += (float)ores;
-      a.y[cr * kTileN + lane] = (_Float16)t;
-    }
-    acc = f4{0.f, 0.f, 0.f, 0.f};
-  };
-  const int64_t rounds = (int64_t)nrow * (a.Kt / PF);
-  for (int64_t rd = 0; rd + 1 < rounds; ++rd) {
-    lkt += PF;
-    if (lkt == a.Kt) {  // wave-uniform: the load cursor moves to the wave's next row
-      lkt = 0;
-      lr += a.nwaves;
-      lqw = a.qw + lr * wrow + lane * BITS;
-      lsz = a.qsz + lr * srow + n_in;
-    }
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      compute(u);
-#ifdef GEMV_ROWS_STAMP
-      if (rd == 0 && u == 0) ROWS_STAMP(3);  // the first tile computed
-#endif
-      load(u);
-    }
-    ckt += PF;
-    if (ckt == a.Kt) {  // wave-uniform: the row is complete
-      store();
-      ckt = 0;
-      cr += a.nwaves;
-      load_epi(cr);
+      a.y[r * kTileN + n] = (_Float16)t;
     }
   }
-#pragma unroll
-  for (int u = 0; u < PF; ++u) compute(u);
-  ROWS_STAMP(4);
-  store();
-  ROWS_STAMP(5);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1156,41 +1183,32 @@ static inline bool group_fast(int K, int group) {  // whole-tile or 32 / 64-wide
   return K % kTileK == 0 && (group % kTileK == 0 || group == 32 || group == 64);
 }
 
-// ---- M == 1, wide matrices: the whole-row kernel ------------------------------------------------
-#ifndef GEMV_WROW_MIN_ROWS_CU  // dev knob: tile rows per CU from which the whole-row kernel runs
-#define GEMV_WROW_MIN_ROWS_CU 4
-#endif
-#ifndef GEMV_WROW_RW  // dev knob: waves (rows in flight) per block; 0 = ceil(rows / CUs)
-#define GEMV_WROW_RW 0
-#endif
-#ifndef GEMV_WROW_PF  // dev knob: tiles in flight per wave (gate/up: 8 15.3 us, 16 17.2 us;
-#define GEMV_WROW_PF 8  // tools/dev/rows_sweep.py, one box)
-#endif
+// ---- M == 1, wide matrices: the work-queue kernel ------------------------------------------------
 struct WrowGeo {
-  int rw, nb, pf;
+  int nb, CPR, max_rows, part_off, sz_off, misc_off, lds;
 };
-// one tile row per wave where the rows fill the CUs (RW = ceil(rows / CU) waves per block, one
-// block per CU), more rows per wave beyond 8 per CU; PF tiles in flight, Kt % PF == 0
-static inline bool wrow_geometry(int64_t Nt, int Kt, int K, WrowGeo& g) {
+// one block per CU for matrices of >= 4 tile rows per CU with whole chunks of k-tiles; the LDS
+// image (x, the partials of every row's chunks, the waves' (scale, zero) slots) within 64 KB
+static inline bool wrow_geometry(int64_t Nt, int Kt, int K, int group, WrowGeo& g) {
   const int64_t cus = device_cu_count();
-  if (Nt < GEMV_WROW_MIN_ROWS_CU * cus) return false;
-  g.pf = Kt % GEMV_WROW_PF == 0 ? GEMV_WROW_PF : (Kt % 8 == 0 ? 8 : 0);
-  if (!g.pf) return false;
-  g.rw = (int)std::min<int64_t>(kWrowMaxWaves, GEMV_WROW_RW > 0 ? GEMV_WROW_RW : (Nt + cus - 1) / cus);
-  g.nb = (int)std::min<int64_t>(cus, (Nt + g.rw - 1) / g.rw);
-  // the x staging covers K / 8 chunks with kWrowXIter per thread
-  return (int64_t)g.rw * 64 * kWrowXIter * 8 >= K;
+  if (Nt < 4 * cus || Kt % kWqC || K > 64 * kWqWaves * 8 * 4) return false;
+  g.nb = (int)std::min<int64_t>(cus, Nt);
+  g.CPR = Kt / kWqC;
+  g.max_rows = (int)((Nt + g.nb - 1) / g.nb);
+  const int GPT = group % kTileK == 0 ? 1 : group == 64 ? 2 : 4;
+  wq_lds_layout(K, g.max_rows, g.CPR, GPT, g.part_off, g.sz_off, g.misc_off, g.lds);
+  return g.lds <= 64 * 1024;
 }
 
 template <int BITS, int GPT, int ZM, int NRM>
 int launch_wrow(const WrowArgs& a, const WrowGeo& g, hipStream_t st) {
-  const size_t lds = (size_t)a.K * 2;
-#define QLIN_WR(P)                                                                             \
-  hipLaunchKernelGGL((gemv_wrow_kernel<BITS, GPT, ZM, P, NRM>), dim3((unsigned)g.nb),           \
-                     dim3(64 * g.rw), lds, st, a)
-  if (g.pf == 16) QLIN_WR(16);
-  else QLIN_WR(8);
-#undef QLIN_WR
+  const int xi = (a.K / 8 + 64 * kWqWaves - 1) / (64 * kWqWaves);
+#define QLIN_WQ(XI)                                                                             \
+  hipLaunchKernelGGL((gemv_wq_kernel<BITS, GPT, ZM, NRM, XI>), dim3((unsigned)g.nb),            \
+                     dim3(64 * kWqWaves), (size_t)g.lds, st, a)
+  if (xi <= 1) QLIN_WQ(1);
+  else QLIN_WQ(4);
+#undef QLIN_WQ
   return (int)hipGetLastError();
 }
 
@@ -1199,9 +1217,6 @@ int launch_wrow_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
                   uint16_t* y, int N, int K, int group, hipStream_t st, int ep,
                   const uint16_t* res, const void* nw, bool nw16, float eps, const WrowGeo& g) {
   WrowArgs a;
-#ifdef GEMV_ROWS_STAMP
-  a.stamps = g_rows_stamps;
-#endif
   a.qw = qw;
   a.qsz = qsz;
   a.x = (const _Float16*)x;
@@ -1218,7 +1233,11 @@ int launch_wrow_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   a.Kt = K / kTileK;
   a.G = K / group;
   a.Nt = (N + kTileN - 1) / kTileN;
-  a.nwaves = g.nb * g.rw;
+  a.nb = g.nb;
+  a.CPR = g.CPR;
+  a.part_off = g.part_off;
+  a.sz_off = g.sz_off;
+  a.misc_off = g.misc_off;
   a.cmagic = tile_group_magic(group);
 #define QLIN_WG(GPT)                                                                            \
   return !nw  ? launch_wrow<BITS, GPT, ZM, 0>(a, g, st)                                         \
@@ -1416,7 +1435,7 @@ static inline int m1_route(int64_t N, int K, int group, const void* x, const voi
   const int64_t Nt = (N + kTileN - 1) / kTileN;
   const int Kt = K / kTileK;
   const bool aligned = ((uintptr_t)x & 15) == 0 && ((uintptr_t)nw & 15) == 0 && K % 8 == 0;
-  if (aligned && wrow_geometry(Nt, Kt, K, wg)) return kM1Wrow;
+  if (aligned && wrow_geometry(Nt, Kt, K, group, wg)) return kM1Wrow;
   if (Nt <= (1 << 26) && fast_geometry((int)Nt, Kt, W, lw, tpw)) return kM1Fast;
   if (rows_geometry(Nt, Kt, rg)) return kM1Rows;
   return kM1None;
