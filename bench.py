@@ -269,10 +269,10 @@ def decode_layer_bench(args, dev, timed):
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s), torch.no_grad():
         step()
-    torch.cuda.current_stream(dev).wait_stream(s)
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph), torch.no_grad():
+    with torch.cuda.graph(graph, stream=s), torch.no_grad():  # capture on the warm-up stream
         step()
+    torch.cuda.current_stream(dev).wait_stream(s)
     steps = max(10, args.steps // 2)
     el, _ = timed(graph.replay, steps, max(2, args.warmup // 2))
     us = el / steps / R * 1e6
@@ -419,10 +419,10 @@ def main():
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             step()  # warm the code objects outside capture
-        torch.cuda.current_stream(dev).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, stream=s):
             step()
+        torch.cuda.current_stream(dev).wait_stream(s)
         return graph.replay
 
     def timed(run, steps, warmup):

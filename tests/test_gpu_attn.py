@@ -63,12 +63,33 @@ def test_attn_decode_split_counters_reset_under_graph_replay():
         with torch.cuda.graph(gr, stream=s):
             out = qlin.attn_decode(q, k, v, None, math.sqrt(128))
         for _ in range(3):
+            out.zero_()
             gr.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(first, out)
     torch.cuda.synchronize()
     assert torch.equal(first, again)
-    assert torch.equal(first, out)
     ref = _ref(q, k, v, None)
     assert (first.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_attn_decode_interleaved_shapes_and_layers():
+    """Many launches of different lengths (split counts) and batch shapes back to back on one
+    stream sharing its merge counters, each checked against the float64 reference (every launch
+    leaves the counters zero for the next)."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    cases = []
+    for L in (513, 1500, 77, 513, 4096, 1500, 600, 513):
+        B = 1 if L != 77 else 3
+        q = torch.randn(B, 32, 1, 128, device="cuda", generator=g)
+        k = torch.randn(B, 8, L, 128, device="cuda", generator=g).half()
+        v = torch.randn(B, 8, L, 128, device="cuda", generator=g).half()
+        cases.append((q, k, v))
+    for rep in range(3):
+        outs = [qlin.attn_decode(q, k, v, None, math.sqrt(128)) for q, k, v in cases]
+        for (q, k, v), o in zip(cases, outs):
+            ref = _ref(q, k, v, None)
+            assert (o.double() - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
 
 
 @pytest.mark.parametrize("B,L,rows", [(1, 513, 1024), (2, 77, 80), (1, 4096, 4104)])

@@ -64,10 +64,10 @@ def main():
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s), torch.no_grad():
             step()
-        torch.cuda.current_stream().wait_stream(s)
         gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr), torch.no_grad():
+        with torch.cuda.graph(gr, stream=s), torch.no_grad():  # capture on the warm-up stream
             out = step()
+        torch.cuda.current_stream().wait_stream(s)
         for _ in range(3):
             gr.replay()
         torch.cuda.synchronize()
