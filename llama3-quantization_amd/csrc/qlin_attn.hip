@@ -43,10 +43,9 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kD = 128;          // head_dim
-#ifndef ATTN_THREADS  // dev A/B knob (tools/dev/Makefile.rows libattn_t<N>.so): 8 waves took
-#define ATTN_THREADS 256  // a cold launch 8.2 -> 7.6 us at L = 513 but the graph-replayed decode
-#endif                    // layer 43.25 -> 43.58 us (same box): 4 waves kept
-constexpr int kThreads = ATTN_THREADS;
+// 4 waves per block: 8 took a cold launch 8.2 -> 7.6 us at L = 513 but the graph-replayed decode
+// layer 43.25 -> 43.58 us (round 4, same box)
+constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxGroup = 8;     // query heads per KV head
 constexpr int kMaxL = 4096;
@@ -55,10 +54,8 @@ constexpr int kRowsU = kThreads / 8;  // K rows per load set (8 lanes per row)
 constexpr int kKU = kSub / kRowsU;    // load sets per pass
 constexpr int kMaxChunk = 512;   // scores of one chunk live in LDS: 512 x 8 fp32 = 16 KB
 constexpr int kMaxSplit = kMaxL / kSub;
-#ifndef ATTN_TARGET_BLOCKS  // dev sweeps (tools/dev/Makefile libattnT<N>.so); round 3: 256
-#define ATTN_TARGET_BLOCKS 256   // (tools/dev/attn_ab.py: L = 4096 17.2 -> 14.7 us, L <= 2048 +-0)
-#endif
-constexpr int kTargetBlocks = ATTN_TARGET_BLOCKS;
+// blocks a launch aims for (round 3 sweep: L = 4096 17.2 -> 14.7 us at 256, L <= 2048 +-0)
+constexpr int kTargetBlocks = 256;
 
 struct Split {
   int chunk, S;
@@ -74,26 +71,14 @@ Split choose_split(int64_t B, int Hkv, int64_t L) {
   return Split{(int)chunk, (int)((L + chunk - 1) / chunk)};
 }
 
-// Dev ablation hook (tools/dev/Makefile libattn<N>.so): 0 = product (sc1 hand-off, see above),
-// 1 = device-scope __threadfence() in every thread instead.
-#ifndef ATTN_FENCE_MODE
-#define ATTN_FENCE_MODE 0
-#endif
-
+// partials cross blocks at agent scope (sc1), acknowledged by vmcnt(0) before the count; a
+// device-scope __threadfence() in every thread instead measured slower (round 3)
 __device__ __forceinline__ void part_store(float* p, float v) {
-#if ATTN_FENCE_MODE == 0
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  *p = v;
-#endif
 }
 
 __device__ __forceinline__ float part_load(const float* p) {
-#if ATTN_FENCE_MODE == 0
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  return *p;
-#endif
 }
 
 template <int CTRL>
@@ -172,23 +157,7 @@ struct AttnArgs {
   RopeIn ri;
   const int* len;  // NULL, or the device-resident cache length (L is then the capacity: the
                    // grid and the partials are sized for it; blocks past the length exit)
-#ifdef ATTN_STAMP
-  uint64_t* stamps;
-#endif
 };
-
-// dev build only (tools/dev/attn_stamps.py): s_memrealtime (100 MHz) per block [block][8] at
-// 0 start, 1 q ready, 2 scores (K landed), 7 softmax statistics, 3 P V (V landed), 4 partials
-// counted, 5 merge inputs loaded, 6 output stored
-#ifdef ATTN_STAMP
-inline uint64_t* g_attn_stamps = nullptr;
-#define AT_STAMP(P, k)                                                                          \
-  if ((P).stamps && threadIdx.x == 0)                                                          \
-  (P).stamps[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] =                      \
-      __builtin_amdgcn_s_memrealtime()
-#else
-#define AT_STAMP(P, k)
-#endif
 
 template <int GRP, bool ROPE = false>
 __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh, const int split) {
@@ -219,7 +188,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   __shared__ float ml_l[kMaxSplit][GRP];   // merge: chunk sums
   __shared__ int last;
 
-  AT_STAMP(A, 0);
   const int b = bh / Hkv, hk = bh % Hkv;  // bh = b * Hkv + kv head
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int sub = tid & 7, tl = tid >> 3;  // score passes: 8 lanes x 16 dims per K row
@@ -340,7 +308,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     }
   }
   __syncthreads();
-  AT_STAMP(A, 1);
 
   // scores (the next pass's K rows are in flight while this pass computes)
   for (int tb = 0; tb < n; tb += kSub) {
@@ -397,7 +364,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     }
   }
   __syncthreads();
-  AT_STAMP(A, 2);
 
   // chunk softmax statistics: wave w owns query heads w, w + 4 (wave-level reductions only)
   for (int g = wave; g < GRP; g += kWaves) {
@@ -417,7 +383,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     }
   }
   __syncthreads();
-  AT_STAMP(A, 7);
 
   // P V: branch-free (rows past the chunk: clamped reads, results selected away), the
   // probabilities of RB rows read from LDS together (one LDS round trip per RB rows, not per row)
@@ -428,10 +393,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
 #pragma unroll
     for (int g = 0; g < GRP; ++g) a0[g] = a1[g] = 0.f;
     const uint32_t vn = has_new ? *reinterpret_cast<const uint32_t*>(&vnew[2 * lane]) : 0u;
-#if defined(ATTN_STAMP) && defined(ATTN_STAMP_VWAIT)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    AT_STAMP(A, 5);  // dev: V landed (slot 5 is free in blocks that do not merge)
-#endif
     for (int tb = 0; tb < n; tb += kSub) {
       uint32_t vc[VR];
 #pragma unroll
@@ -469,7 +430,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     }
   }
   __syncthreads();
-  AT_STAMP(A, 3);
 
   const int64_t qh0 = (int64_t)b * Hq + (int64_t)hk * GRP;  // first query head of the group
   // output row of the group: fp32, or rounded once to fp16 (== the reference's .to(fp16))
@@ -486,7 +446,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
   auto put_all = [&]() {
     for (int o = tid; o < GRP * kD; o += kThreads)
       put(o, wave_total(o) / cl[o / kD]);
-    AT_STAMP(A, 6);
   };
   if (S == 1) {
     put_all();
@@ -501,21 +460,13 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     float* ml = part_ml + ((int64_t)bh * Sl + split) * GRP * 2;
     part_store(ml + tid, (tid & 1) ? cl[tid >> 1] : cm[tid >> 1]);
   }
-#if ATTN_FENCE_MODE == 0
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sc1 stores acknowledged before the count
-#else
-  __threadfence();
-#endif
   __syncthreads();
   if (tid == 0)
     last = (__hip_atomic_fetch_add(&counters[bh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
             S - 1);
   __syncthreads();
-  AT_STAMP(A, 4);
   if (!last) return;
-#if ATTN_FENCE_MODE != 0
-  __threadfence();
-#endif
 
   // merge: the first kPre partial rows of every wave (s = wave + kWaves i) are requested with
   // the chunk statistics — one memory round trip instead of two at decode lengths (S <= 16)
@@ -550,7 +501,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& A, const int bh
     if (lane == 0) cl[g] = den;
   }
   __syncthreads();
-  AT_STAMP(A, 5);
   // weighted sum of the S partial rows: wave w takes rows s = w, w + 4, ...; lane owns floats
   // o = lane + 64 j of the GRP x 128 row (one coalesced 256-B load per wave and j)
   {
@@ -607,9 +557,6 @@ int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const ui
   AttnArgs A{q, (const _Float16*)k, (const _Float16*)v, (const _Float16*)mask, out,
                    out_dtype == QLIN_F16, Hq, Hkv, (int)L, kv_hs, sp.chunk, sp.S, scale_div,
                    (int*)counters, part_o, part_ml, ri, len};
-#ifdef ATTN_STAMP
-  A.stamps = g_attn_stamps;
-#endif
 #define QLIN_A(G, R) \
   hipLaunchKernelGGL((attn_decode_kernel<G, R>), grid, dim3(kThreads), 0, st, A)
 #define QLIN_AR(G)                \
@@ -629,10 +576,6 @@ int launch_decode(const float* q, const uint16_t* k, const uint16_t* v, const ui
 }
 
 }  // namespace
-
-#ifdef ATTN_STAMP
-extern "C" void qlin_dev_attn_stamps(uint64_t* p) { g_attn_stamps = p; }
-#endif
 
 extern "C" int64_t qlin_attn_decode_partials_bytes(int64_t B, int Hq, int Hkv, int64_t L) {
   if (B < 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv || L <= 0 || L > kMaxL) return -1;

@@ -46,11 +46,9 @@ constexpr int kD = 128;       // head_dim
 constexpr int kKB = 64;       // keys per block
 constexpr int kMaxG = 8;      // query heads per KV head
 constexpr float kLog2e = 1.4426950408889634f;
-#ifndef AP_LAZY  // dev switch (tools/dev/Makefile libap<N>.so): 0 = rescale on every new maximum
-#define AP_LAZY 1
-#endif
-// the reference point moves when the row max passes it by this (exp2 units: p 2^12 < 2^15)
-constexpr float kLazy = AP_LAZY ? 3.f : 0.f;
+// the reference point moves when the row max passes it by this (exp2 units: p 2^12 < 2^15;
+// 0 = rescale on every new maximum, measured slower in round 3)
+constexpr float kLazy = 3.f;
 
 struct PrefillArgs {
   const float* q;      // [B, Hq, S, D]

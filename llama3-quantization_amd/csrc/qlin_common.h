@@ -128,6 +128,12 @@ __device__ __forceinline__ uint32_t vreg() {
   asm("v_mov_b32 %0, %1" : "=v"(m) : "i"(C));
   return m;
 }
+// (a & m) | c as one v_and_or_b32, the mask from an SGPR
+__device__ __forceinline__ uint32_t and_or_v(uint32_t a, uint32_t m, uint32_t c) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(c));
+  return r;
+}
 struct Magics {
   uint32_t m1024, m256, m64, m16;
 };
@@ -157,19 +163,21 @@ __device__ __forceinline__ void step_pairs(const Piece<BITS>& c, const Magics& g
     v[1] = ((a >> 8) & 0x00FF00FFu) | g.m1024;
     v[2] = (b & 0x00FF00FFu) | g.m1024;
     v[3] = ((b >> 8) & 0x00FF00FFu) | g.m1024;
-  } else {
+  } else if constexpr (BITS == 2) {
     const uint32_t w = (S & 1) ? (c.w[S >> 1] >> 8) : c.w[S >> 1];
     v[0] = (w & 0x00030003u) | g.m1024;
     v[1] = (w & 0x000C000Cu) | g.m256;
     v[2] = (w & 0x00300030u) | g.m64;
     v[3] = (w & 0x00C000C0u) | g.m16;
-    if constexpr (BITS == 3) {
-      const uint32_t h = (rho3(S) == 0) ? c.w[2] : __builtin_amdgcn_alignbit(c.w[2], c.w[2], rho3(S));
-      v[0] |= h & 0x00040004u;
-      v[1] |= h & 0x00100010u;
-      v[2] |= h & 0x00400040u;
-      v[3] |= h & 0x01000100u;
-    }
+  } else {
+    // int3: the high bit joins the magic first, then the 2-bit field -- two v_and_or_b32 per pair
+    // (left to itself the compiler emits AND, AND, OR3: three)
+    const uint32_t w = (S & 1) ? (c.w[S >> 1] >> 8) : c.w[S >> 1];
+    const uint32_t h = (rho3(S) == 0) ? c.w[2] : __builtin_amdgcn_alignbit(c.w[2], c.w[2], rho3(S));
+    v[0] = and_or_v(w, 0x00030003u, and_or_v(h, 0x00040004u, g.m1024));
+    v[1] = and_or_v(w, 0x000C000Cu, and_or_v(h, 0x00100010u, g.m256));
+    v[2] = and_or_v(w, 0x00300030u, and_or_v(h, 0x00400040u, g.m64));
+    v[3] = and_or_v(w, 0x00C000C0u, and_or_v(h, 0x01000100u, g.m16));
   }
 }
 

@@ -365,24 +365,11 @@ __global__ __launch_bounds__(1024) void gemv_kernel(
 // compiler counts them with vmcnt(N): x words first, then the first PF tiles' codes and
 // (scale, zero) words; the x wait does not wait for the weights.
 // ---------------------------------------------------------------------------------------------
-#ifndef GEMV_ROWS_BPC  // dev knob: resident blocks per CU of a persistent (multi-row) launch
-#define GEMV_ROWS_BPC 2
-#endif
-#ifndef GEMV_ROWS_CONTIG  // dev knob: 1 = wave w takes k-tiles w*TPW .. (w+1)*TPW - 1, 0 = k-tiles
-#define GEMV_ROWS_CONTIG 2  // w, w + W, w + 2W, ...; 2 = contiguous for TPW = 8 only (measured:
-#endif                      // down 8.25 vs 8.39 us contiguous, 4096^2 3.86 vs 4.02 strided)
-#ifndef GEMV_ROWS_MAXPF  // dev knob: most tiles in flight per wave
-#define GEMV_ROWS_MAXPF 8
-#endif
-#ifndef GEMV_ROWS_SZFIRST  // dev knob: 1 = each tile's (scale, zero) words issued before its codes,
-#define GEMV_ROWS_SZFIRST 0  // tile by tile (scheduling barriers keep the order)
-#endif
-#ifndef GEMV_ROWS_SYNC  // dev knob: 1 = __syncthreads() at the row barrier (drains vmcnt)
-#define GEMV_ROWS_SYNC 0
-#endif
-#ifndef GEMV_ROWS_LDS_MIN  // dev knob: dynamic LDS bytes asked of a persistent launch at least
-#define GEMV_ROWS_LDS_MIN 0  // (more than half of the CU's 160 KB admits one block per CU)
-#endif
+// Measured and not kept (round-4 dev builds): (scale, zero) words issued before each tile's
+// codes; __syncthreads() at the row barrier (drains vmcnt); a dynamic-LDS floor admitting one
+// block per CU.  Wave w streams k-tiles w*TPW .. (w+1)*TPW - 1 when TPW = 8 (down 8.25 vs 8.39 us
+// strided), else k-tiles w, w + W, ... (4096^2 3.86 vs 4.02 us contiguous).
+constexpr int kRowsBpc = 2;  // resident blocks per CU of a persistent (multi-row) launch
 constexpr int kRowsMaxTPW = 8;  // k-tiles per wave and row
 
 // NRM (the fused RMSNorm of one token row): 0 none, kNwF32 an fp32 norm weight, kNwF16 the
@@ -422,18 +409,7 @@ struct RowsArgs {
   int nb, rpb, extra;   // blocks; block b owns rpb + (b < extra) tile rows b, b + nb, ...
   int64_t wstep, sstep; // qweight / qsz words between two rows of a block (nb tile rows)
   uint32_t cmagic;      // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
-#ifdef GEMV_ROWS_STAMP  // dev build only: per-wave s_memrealtime stamps [block][wave][8]
-  uint64_t* stamps;
-#endif
 };
-#ifdef GEMV_ROWS_STAMP
-#define ROWS_STAMP(k)                                                                      \
-  if (a.stamps && lane == 0)                                                               \
-    a.stamps[((int64_t)blockIdx.x * kMaxWaves + wave) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
-inline uint64_t* g_rows_stamps = nullptr;  // set by qlin_dev_rows_stamps (dev build)
-#else
-#define ROWS_STAMP(k)
-#endif
 
 template <int BITS, int GPT, int ZM, int TPW, int PF, int NRM>
 __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
@@ -444,10 +420,9 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
   const int b = blockIdx.x;
-  ROWS_STAMP(0);
   const int nrows = a.rpb + (b < a.extra ? 1 : 0);
   const int T = nrows * TPW;  // tiles this wave streams (host: T >= PF)
-  constexpr bool kContig = GEMV_ROWS_CONTIG == 2 ? TPW >= 8 : GEMV_ROWS_CONTIG != 0;
+  constexpr bool kContig = TPW >= 8;
   const int kt0 = kContig ? wave * TPW : wave;
   const int kts = kContig ? 1 : a.W;
   auto group_of_tile = [&](int kt) {
@@ -491,16 +466,9 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
   auto load = [&](int u) {
     const int ki = il * kts;  // k-tile offset from kt0
     const int g0 = group_of_tile(kt0 + ki);
-    if (GEMV_ROWS_SZFIRST) {
+    wt[u].pc = load_piece_nt<BITS>(qwp + lq + ki * (64 * BITS));
 #pragma unroll
-      for (int s = 0; s < GPT; ++s) wt[u].sz[s] = szp[ls + (g0 + s) * kTileN];
-      wt[u].pc = load_piece_nt<BITS>(qwp + lq + ki * (64 * BITS));
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      wt[u].pc = load_piece_nt<BITS>(qwp + lq + ki * (64 * BITS));
-#pragma unroll
-      for (int s = 0; s < GPT; ++s) wt[u].sz[s] = szp[ls + (g0 + s) * kTileN];
-    }
+    for (int s = 0; s < GPT; ++s) wt[u].sz[s] = szp[ls + (g0 + s) * kTileN];
     if (++il == TPW) {
       il = 0;
       lq += a.wstep;
@@ -510,7 +478,6 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u);
 
-  ROWS_STAMP(1);
 
   if constexpr (NRM) {
 #pragma clang fp contract(off)
@@ -541,7 +508,6 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
   uint32_t* xsl = &xs[wave][0];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) xsl[i * 64 + lane] = xw[i];
-  ROWS_STAMP(2);
 
   const Magics mg = make_magics<BITS>();
   f4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -549,8 +515,7 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
   auto epilogue = [&]() {
     if (lane < kTileN) red[par][lane][wave] = acc[0];
     acc = f4{0.f, 0.f, 0.f, 0.f};
-    if (GEMV_ROWS_SYNC) __syncthreads();
-    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (wave == ew) {  // wave-uniform
       const int64_t r = (int64_t)b + (int64_t)jc * a.nb;
       auto total = [&](int n, _Float16 bv) {  // the W partials in a fixed tree order
@@ -597,13 +562,7 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
     step(std::integral_constant<int, 1>{});
     step(std::integral_constant<int, 2>{});
     step(std::integral_constant<int, 3>{});
-#ifdef GEMV_ROWS_STAMP
-    if (jc == 0 && ic == 0) ROWS_STAMP(3);  // the first tile computed
-#endif
     if (++ic == TPW) {  // block-uniform: the row is complete in every wave
-#ifdef GEMV_ROWS_STAMP
-      if (jc + 1 == nrows) ROWS_STAMP(4);  // the last tile computed
-#endif
       epilogue();
       ic = 0;
       ++jc;
@@ -628,7 +587,6 @@ __global__ __launch_bounds__(1024) void gemv_rows_kernel(const RowsArgs a) {
 #pragma unroll
   for (int u = 0; u < PF; ++u)
     if (u < rem) compute(u);
-  ROWS_STAMP(5);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1137,12 +1095,10 @@ static inline uint32_t tile_group_magic(int group) {  // GPT == 1: kt / (group /
 // >= 512 row tiles keep >= 4 tiles per wave (measured on the decode layer's shapes,
 // tools/dev/gemv_geo.py: 28,672 x 4,096 W = 8 12.6 us vs W = 4 13.3 us; 14,336 x 4,096 W = 8
 // 8.9 us vs W = 16 9.3 us; 4096 x 4096 and 6144 x 4096 keep W = 16)
-#ifndef GEMV_WAVE_TARGET  // dev sweep knob (tools/dev/Makefile libgv*.so)
-#define GEMV_WAVE_TARGET 8192
-#endif
+constexpr int64_t kWaveTarget = 8192;
 static inline int pick_waves(int Nt, int Kt, int& tpw) {
   int W = 1;
-  while (W < kMaxWaves && (int64_t)Nt * W < GEMV_WAVE_TARGET && (Nt < 512 || Kt >= 8 * W)) W *= 2;
+  while (W < kMaxWaves && (int64_t)Nt * W < kWaveTarget && (Nt < 512 || Kt >= 8 * W)) W *= 2;
   W = min(W, Kt);
   tpw = (Kt + W - 1) / W;
   return (Kt + tpw - 1) / tpw;
@@ -1256,21 +1212,17 @@ struct RowsGeo {
 
 // W * TPW == Kt with TPW the smallest of {2, 4, 8} that keeps W <= 16 (the most waves per row);
 // one row per block up to 2 rows per CU (PF = the wave's whole row), else a persistent grid of
-// GEMV_ROWS_BPC blocks per CU streaming 8 tiles ahead across rows
-#ifndef GEMV_ROWS_MINTPW  // dev knob: smallest k-tiles per wave and row
-#define GEMV_ROWS_MINTPW 2
-#endif
-#ifndef GEMV_ROWS_ONEROW_CU  // dev knob: grids of up to this many rows per CU run one row per block
-#define GEMV_ROWS_ONEROW_CU 2
-#endif
+// kRowsBpc blocks per CU streaming 8 tiles ahead across rows
+constexpr int kRowsMinTPW = 2;   // smallest k-tiles per wave and row
+constexpr int kRowsOneRowCU = 2; // grids of up to this many rows per CU run one row per block
 static inline bool rows_geometry(int64_t Nt, int Kt, RowsGeo& g) {
   const int64_t cus = device_cu_count();
   // one-row grids: few enough waves that every block is resident at once (16 waves per CU: the
   // register budget of these kernels admits at least that); measured qkv (384 rows) W = 16: two
-  // rounds of blocks, 7.4 us; W = 8: 6.1 us (tools/dev/rows_stamps.py, rows_sweep.py)
-  const bool onerow = Nt <= GEMV_ROWS_ONEROW_CU * cus;
+  // rounds of blocks, 7.4 us; W = 8: 6.1 us (round-4 stamp builds)
+  const bool onerow = Nt <= kRowsOneRowCU * cus;
   g.TPW = 0;
-  for (int t = GEMV_ROWS_MINTPW; t <= kRowsMaxTPW; t *= 2)
+  for (int t = kRowsMinTPW; t <= kRowsMaxTPW; t *= 2)
     if (Kt % t == 0 && Kt / t <= kMaxWaves && (!onerow || t == kRowsMaxTPW ||
                                                Nt * (Kt / t) <= kMaxWaves * cus)) {
       g.TPW = t;
@@ -1278,16 +1230,15 @@ static inline bool rows_geometry(int64_t Nt, int Kt, RowsGeo& g) {
     }
   if (!g.TPW || Nt < 1 || Nt > (1 << 26)) return false;
   g.W = Kt / g.TPW;
-  g.nb = onerow ? (int)Nt : (int)(cus * GEMV_ROWS_BPC);
-  g.pf = (g.nb < Nt && GEMV_ROWS_MAXPF >= 8 && (Nt / g.nb) * g.TPW >= 8) ? 8 : g.TPW;
+  g.nb = onerow ? (int)Nt : (int)(cus * kRowsBpc);
+  g.pf = (g.nb < Nt && (Nt / g.nb) * g.TPW >= 8) ? 8 : g.TPW;
   return true;
 }
 
 
 template <int BITS, int GPT, int ZM, int NRM>
 int launch_rows(const RowsArgs& a, const RowsGeo& g, hipStream_t st) {
-  size_t lds = 0;
-  if (g.nb < a.N / kTileN && GEMV_ROWS_LDS_MIN > 0) lds = GEMV_ROWS_LDS_MIN;
+  const size_t lds = 0;
 #define QLIN_GR(T, P)                                                                          \
   hipLaunchKernelGGL((gemv_rows_kernel<BITS, GPT, ZM, T, P, NRM>), dim3((unsigned)g.nb),        \
                      dim3(64 * g.W), lds, st, a)
@@ -1334,9 +1285,6 @@ int launch_rows_g(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
   a.wstep = (int64_t)g.nb * a.Kt * 64 * BITS;
   a.sstep = (int64_t)g.nb * a.G * kTileN;
   a.cmagic = tile_group_magic(group);
-#ifdef GEMV_ROWS_STAMP
-  a.stamps = g_rows_stamps;
-#endif
 #define QLIN_RG(GPT)                                                                            \
   return !nw  ? launch_rows<BITS, GPT, ZM, 0>(a, g, st)                                         \
          : nw16 ? launch_rows<BITS, GPT, ZM, kNwF16>(a, g, st)                                  \
@@ -1373,7 +1321,7 @@ int launch_fast_t(const FastArgs& a, bool nw16, int Nt, int tpw, hipStream_t st)
 
 // fast-path geometry: pick_waves rounded down to a power of two, then halved while the grid holds
 // more than 16 waves per CU (all blocks resident in one round: q/k/v, 384 row tiles, W = 16 ran in
-// two rounds, tools/dev/rows_stamps.py); the fast path takes launches whose waves stream at most 4
+// two rounds, round-4 stamp builds); the fast path takes launches whose waves stream at most 4
 // tiles (tools/dev/fast_geo.py)
 static inline bool fast_geometry(int Nt, int Kt, int& W, int& lw, int& tpw) {
   W = pick_waves(Nt, Kt, tpw);
@@ -1638,10 +1586,6 @@ extern "C" int qlin_rmsnorm_linear_ep_f16(const uint32_t* qweight, const uint32_
   }
 #undef QLIN_N
 }
-
-#ifdef GEMV_ROWS_STAMP
-extern "C" void qlin_dev_rows_stamps(uint64_t* p) { qlin_gv::g_rows_stamps = p; }
-#endif
 
 extern "C" int qlin_gemv_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
                              const uint16_t* x, const uint16_t* bias, uint16_t* y, int64_t M,

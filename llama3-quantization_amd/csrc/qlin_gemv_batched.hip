@@ -47,27 +47,8 @@ struct StreamArgs {
 };
 
 constexpr int kStreamWaves = 4;
-#ifndef GEMV_STREAM_PF  // tiles in flight per wave (dev knob)
-#define GEMV_STREAM_PF 8
-#endif
-#ifndef GEMV_STREAM_ABLATE  // dev ablation (wrong results): 1 = no x loads / LDS park, 2 = constant
-#define GEMV_STREAM_ABLATE 0  // (scale, zero) words (loads and group decode folded), 3 = both
-#endif
-#ifndef GEMV_STREAM_SZR  // round-wide (scale, zero) loads (dev A/B knob)
-#define GEMV_STREAM_SZR 1
-#endif
-#ifndef GEMV_STREAM_PFS  // tiles in flight per wave for 2/3-bit tiles (dev knob)
-#define GEMV_STREAM_PFS 8
-#endif
-#ifndef GEMV_STREAM_WPE_SUB  // minimum waves per SIMD asked of the 2/3-bit instances (dev knob;
-#define GEMV_STREAM_WPE_SUB 1   // 1 = compiler's choice)
-#endif
-#ifndef GEMV_STREAM_INTERLEAVE  // dev A/B knob: 1 = wave w takes tile rows w, w + Wt, ...
-#define GEMV_STREAM_INTERLEAVE 0
-#endif
-#ifndef GEMV_STREAM_PERSIST  // dev A/B knob: 0 = one tile row per wave (grid of T waves)
-#define GEMV_STREAM_PERSIST 1
-#endif
+constexpr int kStreamPF = 8;  // tiles in flight per wave (16 for the 2/3-bit tiles,
+                              // 6 or 8 waves per SIMD forced, measured slower)
 
 // SZR (group = 128 / GPT, i.e. 32, 64 or 128): the (scale, zero) words of a whole round of PF
 // tiles -- PF * GPT groups x 16 rows, contiguous in the qsz layout -- arrive as ONE 16-B-per-lane
@@ -75,14 +56,40 @@ constexpr int kStreamWaves = 4;
 // where each k-step reads its lane's word, instead of GPT 64-byte loads per tile: fewer vector
 // memory instructions per tile (int2 g64: 4 -> 2 + 1/round).  tools/dev/batch_geo.py, one box,
 // best of 3: int2 g64 131 -> 125 us, int3 g64 116 -> 115, int4 g128 97.9 -> 96.7 (bit-identical).
+// PRE (SZR with narrow int16 zeros): the group constants are formed once per round, when the
+// round's (scale, zero) words are parked, instead of once per tile and group in every lane: the
+// parked slot holds three planes of SW words -- (s, s), (z + off_0, z + off_1), (z + off_2,
+// z + off_3) in fp16 (off_P = pair_off<BITS>(P); the sums are exact, |z| <= 1024) -- and a k-step
+// reads its lane's words and subtracts the half its pair needs (op_sel), so the per-pair work is
+// the extract, the zero subtraction and the scale multiply alone: the same fp16 operations on the
+// same values as dequant_step (bit-identical): 62.5 -> 52.4 VALU per int2 g64 tile, 99 -> 73 for
+// int3 with two v_and_or_b32 per pair (step_pairs).  tools/dev/batch_geo.py, one box, best of 3:
+// int2 g64 129.9 -> 126.0 us per 96-matrix ring (119.8 with the int3 build), int3 g64 120.2 ->
+// 108.8 us per 64; int4 g128 +-1 %.
+template <int BITS, int S>
+__device__ __forceinline__ void dequant_step_pre(const Piece<BITS>& c, const Magics& mg,
+                                                 uint32_t ssw, uint32_t za, uint32_t zb,
+                                                 uint32_t (&out)[4]) {
+#pragma clang fp contract(off)
+  uint32_t v[4];
+  step_pairs<BITS, S>(c, mg, v);
+  const h2 ss = as_h2(ssw), ha = as_h2(za), hb = as_h2(zb);
+#pragma unroll
+  for (int P = 0; P < 4; ++P) {
+    const h2 zs = (BITS >= 4 || P < 2) ? ha : hb;
+    const _Float16 z = (BITS == 8 || (P & 1) == 0) ? zs.x : zs.y;
+    out[P] = as_u32((as_h2(v[P]) - h2{z, z}) * ss);
+  }
+}
+
 template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
-__global__ __launch_bounds__(64 * kStreamWaves)
-__attribute__((amdgpu_waves_per_eu(BITS < 4 ? GEMV_STREAM_WPE_SUB : 1)))
-void gemv_stream_kernel(const StreamArgs a) {
+__global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[kStreamWaves][64 * MT];
   constexpr int SW = PF * GPT * kTileN;         // SZR: (scale, zero) words per round
   constexpr int NC = SW >= 256 ? SW / 256 : 1;  // 16-B loads per lane per round
-  __shared__ __attribute__((aligned(16))) uint32_t szs[SZR ? kStreamWaves : 1][SZR ? SW : 4];
+  constexpr bool PRE = SZR && ZM == kZNarrow;
+  constexpr int NPL = PRE ? (BITS < 4 ? 3 : 2) : 1;  // parked planes
+  __shared__ __attribute__((aligned(16))) uint32_t szs[SZR ? kStreamWaves : 1][SZR ? NPL * SW : 4];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, n_in = lane & 15;
@@ -90,11 +97,10 @@ void gemv_stream_kernel(const StreamArgs a) {
   if (a.xcd_chunk > 0) blk = (blk & 7) * a.xcd_chunk + (blk >> 3);  // XCD j: a contiguous run
   const int64_t w = (int64_t)blk * kStreamWaves + wave;
   if (w >= a.Wt) return;  // wave-uniform; no barriers below
-  // tile rows of this wave: contiguous [wT/Wt, (w+1)T/Wt), or (dev knob) w, w + Wt, w + 2 Wt, ...
-  const int64_t rstep = GEMV_STREAM_INTERLEAVE ? a.Wt : 1;
-  const int64_t r0 = GEMV_STREAM_INTERLEAVE ? w : w * a.T / a.Wt;
-  const int64_t nrows = GEMV_STREAM_INTERLEAVE ? (a.T - w + a.Wt - 1) / a.Wt
-                                               : (w + 1) * a.T / a.Wt - r0;
+  // tile rows of this wave: contiguous [wT/Wt, (w+1)T/Wt) (an interleaved w, w + Wt, ... measured
+  // within noise, round 3)
+  const int64_t r0 = w * a.T / a.Wt;
+  const int64_t nrows = (w + 1) * a.T / a.Wt - r0;
   if (nrows <= 0) return;
   constexpr int LPR = 64 / MT;
   const int xlane = min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
@@ -129,7 +135,25 @@ void gemv_stream_kernel(const StreamArgs a) {
   };
   uint32_t* sslot = &szs[SZR ? wave : 0][0];
   auto park_sz = [&] {
-    if constexpr (SZR) {
+    if constexpr (PRE) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint32_t ws[4] = {szr[c].x, szr[c].y, szr[c].z, szr[c].w};
+        uint32_t pl[3][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const _Float16 s = sz_scale(ws[e]);
+          const _Float16 z = (_Float16)(int16_t)(ws[e] >> 16);
+          pl[0][e] = as_u32(h2{s, s});
+          pl[1][e] = as_u32(h2{z, z} + h2{(_Float16)pair_off<BITS>(0), (_Float16)pair_off<BITS>(1)});
+          pl[2][e] = as_u32(h2{z, z} + h2{(_Float16)pair_off<BITS>(2), (_Float16)pair_off<BITS>(3)});
+        }
+        const int o = 256 * c + (4 * lane) % (SW < 256 ? SW : 256);
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+          *reinterpret_cast<uint4*>(sslot + p * SW + o) = make_uint4(pl[p][0], pl[p][1], pl[p][2], pl[p][3]);
+      }
+    } else if constexpr (SZR) {
 #pragma unroll
       for (int c = 0; c < NC; ++c)
         *reinterpret_cast<uint4*>(sslot + 256 * c + (4 * lane) % (SW < 256 ? SW : 256)) = szr[c];
@@ -140,13 +164,7 @@ void gemv_stream_kernel(const StreamArgs a) {
     if constexpr (!SZR) {
       const int g0 = group_of_tile(kt);
 #pragma unroll
-      for (int s = 0; s < GPT; ++s)
-        wt[u].sz[s] = (GEMV_STREAM_ABLATE & 2) ? 0x3c000004u + (uint32_t)s : lsz[(g0 + s) * kTileN];
-    }
-    if (GEMV_STREAM_ABLATE & 1) {
-#pragma unroll
-      for (int c = 0; c < MT; ++c) xq[u].w[c] = 0x3c003c00u + (uint32_t)kt;
-      return;
+      for (int s = 0; s < GPT; ++s) wt[u].sz[s] = lsz[(g0 + s) * kTileN];
     }
     const _Float16* p = lx + kt * kTileK;
     if constexpr (MT == 1) {
@@ -164,20 +182,19 @@ void gemv_stream_kernel(const StreamArgs a) {
   uint32_t* slot = &xs[wave][0];
   auto tile = [&](int u) {
     h8 xa[4];
-    if (GEMV_STREAM_ABLATE & 1) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        xa[c] = __builtin_bit_cast(h8, make_uint4(xq[u].w[0], xq[u].w[0] + c, xq[u].w[0], 0u));
-    } else {
-      park_x<MT>(xa, xq[u], slot, lane, n_in);
-    }
+    park_x<MT>(xa, xq[u], slot, lane, n_in);
     auto step = [&](auto S_) {
       constexpr int S = decltype(S_)::value;
       uint32_t v[4];
-      const uint32_t szw =
-          SZR ? sslot[(u * GPT + S * GPT / 4) * kTileN + n_in] : wt[u].sz[S * GPT / 4];
-      const GroupQ gq = make_group_w<BITS, ZM>(szw);
-      dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
+      const int si = (u * GPT + S * GPT / 4) * kTileN + n_in;
+      if constexpr (PRE) {
+        dequant_step_pre<BITS, S>(wt[u].pc, mg, sslot[si], sslot[SW + si],
+                                  NPL > 2 ? sslot[(NPL - 1) * SW + si] : 0u, v);
+      } else {
+        const uint32_t szw = SZR ? sslot[si] : wt[u].sz[S * GPT / 4];
+        const GroupQ gq = make_group_w<BITS, ZM>(szw);
+        dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
+      }
       const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
     };
@@ -217,7 +234,7 @@ void gemv_stream_kernel(const StreamArgs a) {
     lkt += PF;
     if (lkt == a.Kt) {  // wave-uniform
       lkt = 0;
-      lr += rstep;
+      ++lr;
       set_row(lr);
     }
     load_szr(lkt);
@@ -230,7 +247,7 @@ void gemv_stream_kernel(const StreamArgs a) {
     if (ckt == a.Kt) {  // wave-uniform: the tile row is complete
       store(cr);
       ckt = 0;
-      cr += rstep;
+      ++cr;
     }
   }
   park_sz();
@@ -255,9 +272,10 @@ int blocks_per_cu(Kern k) {
 template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
 int launch_stream_pf(StreamArgs a, hipStream_t st) {
   auto k = gemv_stream_kernel<BITS, MT, GPT, ZM, PF, SZR>;
-  int64_t Wt = a.T;
-  if (GEMV_STREAM_PERSIST)
-    Wt = std::min<int64_t>(a.T, (int64_t)device_cu_count() * blocks_per_cu(k) * kStreamWaves);
+  // persistent: the grid is the resident capacity (one tile row per wave, a grid of T waves, ran
+  // its last round with a third of the loads in flight)
+  const int64_t Wt =
+      std::min<int64_t>(a.T, (int64_t)device_cu_count() * blocks_per_cu(k) * kStreamWaves);
   a.Wt = Wt;
   const int64_t blocks = (Wt + kStreamWaves - 1) / kStreamWaves;
   a.xcd_chunk = blocks % 8 == 0 ? (int)(blocks / 8) : 0;
@@ -265,23 +283,18 @@ int launch_stream_pf(StreamArgs a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// tiles in flight per wave: GEMV_STREAM_PF for int4 / int8, GEMV_STREAM_PFS for the 2/3-bit tiles
-// (half / three quarters of the bytes per tile; 16 measured 5-10 % slower than 8 for them:
-// 8 more VGPR slots cost a wave per SIMD)
+// kStreamPF tiles in flight per wave, 4 when K is not a multiple of 8 tiles (Kt % 4 == 0: host)
 template <int BITS, int MT, int GPT, int ZM, bool SZR>
 int launch_stream_s(const StreamArgs& a, hipStream_t st) {
-  constexpr int PF = BITS >= 4 ? GEMV_STREAM_PF : GEMV_STREAM_PFS;
-  if (a.Kt % PF == 0) return launch_stream_pf<BITS, MT, GPT, ZM, PF, SZR>(a, st);
-  if (PF > 8 && a.Kt % 8 == 0) return launch_stream_pf<BITS, MT, GPT, ZM, 8, SZR>(a, st);
-  return launch_stream_pf<BITS, MT, GPT, ZM, 4, SZR>(a, st);  // Kt % 4 == 0 (host)
+  if (a.Kt % kStreamPF == 0) return launch_stream_pf<BITS, MT, GPT, ZM, kStreamPF, SZR>(a, st);
+  return launch_stream_pf<BITS, MT, GPT, ZM, 4, SZR>(a, st);
 }
 
 // group = 128 / GPT: round-wide (scale, zero) loads; GPT == 1 with group > 128 (a multiple of
 // 128, per-channel included): per-tile loads (one group covers several tiles)
 template <int BITS, int MT, int GPT, int ZM>
 int launch_stream_t(const StreamArgs& a, hipStream_t st) {
-  if (GEMV_STREAM_SZR && (GPT > 1 || a.K / a.G == kTileK))
-    return launch_stream_s<BITS, MT, GPT, ZM, GEMV_STREAM_SZR != 0>(a, st);
+  if (GPT > 1 || a.K / a.G == kTileK) return launch_stream_s<BITS, MT, GPT, ZM, true>(a, st);
   return launch_stream_s<BITS, MT, GPT, ZM, false>(a, st);
 }
 
