@@ -121,18 +121,17 @@ template <int BITS> __host__ __device__ constexpr int pair_off(int P) {
 }
 
 // An fp16-pair constant kept in a VGPR.  gfx9 VOP3 has no literal operand, so with the constant
-// opaque to the optimiser `(w & mask) | magic` selects ONE v_and_or_b32 (mask from an SGPR).
+// opaque to the optimiser `(w & mask) | magic` selects ONE v_and_or_b32 (mask from an SGPR).  The
+// value is pinned by an EMPTY asm with a VGPR constraint: no instruction comes from asm, so the
+// compiler's hazard recognizer sees every instruction it schedules (an asm-emitted VALU write is
+// opaque to it -- e.g. the wait states before overwriting an in-flight MFMA's source registers).
+__device__ __forceinline__ uint32_t pin_v(uint32_t x) {
+  asm("" : "+v"(x));
+  return x;
+}
 template <uint32_t C>
 __device__ __forceinline__ uint32_t vreg() {
-  uint32_t m;
-  asm("v_mov_b32 %0, %1" : "=v"(m) : "i"(C));
-  return m;
-}
-// (a & m) | c as one v_and_or_b32, the mask from an SGPR
-__device__ __forceinline__ uint32_t and_or_v(uint32_t a, uint32_t m, uint32_t c) {
-  uint32_t r;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(c));
-  return r;
+  return pin_v(C);
 }
 struct Magics {
   uint32_t m1024, m256, m64, m16;
@@ -170,14 +169,14 @@ __device__ __forceinline__ void step_pairs(const Piece<BITS>& c, const Magics& g
     v[2] = (w & 0x00300030u) | g.m64;
     v[3] = (w & 0x00C000C0u) | g.m16;
   } else {
-    // int3: the high bit joins the magic first, then the 2-bit field -- two v_and_or_b32 per pair
-    // (left to itself the compiler emits AND, AND, OR3: three)
+    // int3: the high bit joins the magic first (pinned, so it is not re-associated), then the
+    // 2-bit field -- two v_and_or_b32 per pair (left to itself the compiler emits AND, AND, OR3)
     const uint32_t w = (S & 1) ? (c.w[S >> 1] >> 8) : c.w[S >> 1];
     const uint32_t h = (rho3(S) == 0) ? c.w[2] : __builtin_amdgcn_alignbit(c.w[2], c.w[2], rho3(S));
-    v[0] = and_or_v(w, 0x00030003u, and_or_v(h, 0x00040004u, g.m1024));
-    v[1] = and_or_v(w, 0x000C000Cu, and_or_v(h, 0x00100010u, g.m256));
-    v[2] = and_or_v(w, 0x00300030u, and_or_v(h, 0x00400040u, g.m64));
-    v[3] = and_or_v(w, 0x00C000C0u, and_or_v(h, 0x01000100u, g.m16));
+    v[0] = (w & 0x00030003u) | pin_v((h & 0x00040004u) | g.m1024);
+    v[1] = (w & 0x000C000Cu) | pin_v((h & 0x00100010u) | g.m256);
+    v[2] = (w & 0x00300030u) | pin_v((h & 0x00400040u) | g.m64);
+    v[3] = (w & 0x00C000C0u) | pin_v((h & 0x01000100u) | g.m16);
   }
 }
 
@@ -345,16 +344,22 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 // v_permlane32_swap / v_permlane16_swap (gfx950): x <-> y exchanges across the wave halves / the
-// odd and even 16-lane rows, VALU only (no LDS round trip).  Inline asm: with both operands the
-// same value, hipcc (ROCm 7.2) folds the builtin's two results into one
-// (tools/dev/probe/permlane.hip); the s_nop covers the VALU-write -> permlane-read hazard.
+// odd and even 16-lane rows, VALU only (no LDS round trip).  With both operands the same value
+// hipcc (ROCm 7.2) folds the builtin's two results into one, so y is an opaque copy (pin_v, an
+// empty asm: the swap itself and its hazard wait states come from the compiler).
 // After permlane32_swap(x, y) with x = y = v: x = v[l % 32], y = v[l % 32 + 32]; after
 // permlane16_swap likewise for the even / odd row of each pair of 16-lane rows.
 __device__ __forceinline__ void permlane32_swap(float& x, float& y) {
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, x),
+                                                  pin_v(__builtin_bit_cast(uint32_t, y)), false, false);
+  x = __builtin_bit_cast(float, (uint32_t)r[0]);
+  y = __builtin_bit_cast(float, (uint32_t)r[1]);
 }
 __device__ __forceinline__ void permlane16_swap(float& x, float& y) {
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, x),
+                                                  pin_v(__builtin_bit_cast(uint32_t, y)), false, false);
+  x = __builtin_bit_cast(float, (uint32_t)r[0]);
+  y = __builtin_bit_cast(float, (uint32_t)r[1]);
 }
 // sum over lanes n, n + 16, n + 32, n + 48 (every lane gets its column's total)
 __device__ __forceinline__ float cols4_sum(float v) {

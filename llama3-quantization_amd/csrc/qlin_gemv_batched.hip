@@ -82,10 +82,19 @@ __device__ __forceinline__ void dequant_step_pre(const Piece<BITS>& c, const Mag
   }
 }
 
-template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
+// NR tile rows side by side (NR = 2: rows 2p, 2p + 1 of one problem; M = 1 with the per-round
+// group constants): every x fragment is parked and read once per k-tile for both rows and each
+// round covers PF / NR k-tiles of both rows, so PF tiles stay in flight.  Each row keeps its own
+// MFMA chain in k order (bit-identical).  tools/dev/stream_lab.hip (`lab2_kernel`), same box:
+// int2 g64 119.3 -> 115.0 us per 96-matrix ring, int3 g64 107.8 -> 105.4, int4 g128 97.6 -> 96.2,
+// at 4 waves per SIMD (see pad_lds_to).
+template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR, int NR>
 __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const StreamArgs a) {
+  static_assert(NR == 1 || (MT == 1 && SZR && ZM == kZNarrow), "two rows: M = 1, narrow zeros");
+  constexpr int PFK = PF / NR;                   // k-tiles per round
   __shared__ __attribute__((aligned(16))) uint32_t xs[kStreamWaves][64 * MT];
-  constexpr int SW = PF * GPT * kTileN;         // SZR: (scale, zero) words per round
+  constexpr int SWR = PFK * GPT * kTileN;       // SZR: (scale, zero) words per row and round
+  constexpr int SW = NR * SWR;                  // ... of all NR rows
   constexpr int NC = SW >= 256 ? SW / 256 : 1;  // 16-B loads per lane per round
   constexpr bool PRE = SZR && ZM == kZNarrow;
   constexpr int NPL = PRE ? (BITS < 4 ? 3 : 2) : 1;  // parked planes
@@ -97,40 +106,45 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
   if (a.xcd_chunk > 0) blk = (blk & 7) * a.xcd_chunk + (blk >> 3);  // XCD j: a contiguous run
   const int64_t w = (int64_t)blk * kStreamWaves + wave;
   if (w >= a.Wt) return;  // wave-uniform; no barriers below
-  // tile rows of this wave: contiguous [wT/Wt, (w+1)T/Wt) (an interleaved w, w + Wt, ... measured
-  // within noise, round 3)
-  const int64_t r0 = w * a.T / a.Wt;
-  const int64_t nrows = (w + 1) * a.T / a.Wt - r0;
+  // row units (NR tile rows each) of this wave: contiguous [wU/Wt, (w+1)U/Wt) (an interleaved
+  // w, w + Wt, ... measured within noise, round 3)
+  const int64_t U = a.T / NR;
+  const int64_t r0 = w * U / a.Wt;
+  const int64_t nrows = (w + 1) * U / a.Wt - r0;
   if (nrows <= 0) return;
   constexpr int LPR = 64 / MT;
   const int xlane = min(lane / LPR, a.M - 1) * a.K + 2 * MT * (lane % LPR);
 
-  // load stream: tile row lr, round start lkt, its operand bases
+  // load stream: row unit lr, round start lkt, its operand bases
   int64_t lr = r0;
   int lkt = 0;
   const uint32_t* lqw;
-  const uint32_t* lsz;   // SZR: the row tile's qsz base; else + n_in
+  const uint32_t* lsz;   // SZR: the unit's first row tile's qsz base; else + n_in
   const _Float16* lx;
-  auto set_row = [&](int64_t r) {
+  const int64_t rw = (int64_t)a.Kt * (64 * BITS), rs = (int64_t)a.G * kTileN;  // per tile row
+  auto set_row = [&](int64_t u) {
+    const int64_t r = u * NR;
     const int64_t b = r / a.Nt;
     const int nt = (int)(r - b * a.Nt);
-    lqw = a.qw + b * a.bs_qw + (int64_t)nt * a.Kt * (64 * BITS) + lane * BITS;
-    lsz = a.qsz + b * a.bs_sz + (int64_t)nt * a.G * kTileN + (SZR ? 0 : n_in);
+    lqw = a.qw + b * a.bs_qw + (int64_t)nt * rw + lane * BITS;
+    lsz = a.qsz + b * a.bs_sz + (int64_t)nt * rs + (SZR ? 0 : n_in);
     lx = a.x + b * a.bs_x + xlane;
   };
   set_row(lr);
   auto group_of_tile = [&](int kt) {
     return GPT == 1 ? (int)(((uint64_t)(uint32_t)kt * a.cmagic) >> 31) : kt * GPT;
   };
-  WTile<BITS, GPT> wt[PF];
-  XRaw<MT> xq[PF];
+  WTile<BITS, GPT> wt[NR][PFK];
+  XRaw<MT> xq[PFK];
   uint4 szr[NC];  // SZR: the next round's (scale, zero) words, lane l: words 4l .. 4l + 3
-  auto load_szr = [&](int kt0) {  // round starting at tile kt0: groups kt0 * GPT ..
+  auto load_szr = [&](int kt0) {  // round starting at tile kt0: groups kt0 * GPT .. of each row
     if constexpr (SZR) {
-      const uint32_t* p = lsz + kt0 * GPT * kTileN;
 #pragma unroll
-      for (int c = 0; c < NC; ++c)
-        szr[c] = *reinterpret_cast<const uint4*>(p + 256 * c + (4 * lane) % (SW < 256 ? SW : 256));
+      for (int c = 0; c < NC; ++c) {
+        const int o = 256 * c + (4 * lane) % (SW < 256 ? SW : 256);
+        const int rr = o / SWR;
+        szr[c] = *reinterpret_cast<const uint4*>(lsz + rr * rs + kt0 * GPT * kTileN + (o - rr * SWR));
+      }
     }
   };
   uint32_t* sslot = &szs[SZR ? wave : 0][0];
@@ -160,11 +174,14 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
     }
   };
   auto load = [&](int u, int kt) {
-    wt[u].pc = load_piece_nt<BITS>(lqw + kt * (64 * BITS));
-    if constexpr (!SZR) {
-      const int g0 = group_of_tile(kt);
 #pragma unroll
-      for (int s = 0; s < GPT; ++s) wt[u].sz[s] = lsz[(g0 + s) * kTileN];
+    for (int rr = 0; rr < NR; ++rr) {
+      wt[rr][u].pc = load_piece_nt<BITS>(lqw + rr * rw + kt * (64 * BITS));
+      if constexpr (!SZR) {
+        const int g0 = group_of_tile(kt);
+#pragma unroll
+        for (int s = 0; s < GPT; ++s) wt[rr][u].sz[s] = lsz[rr * rs + (g0 + s) * kTileN];
+      }
     }
     const _Float16* p = lx + kt * kTileK;
     if constexpr (MT == 1) {
@@ -178,60 +195,69 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
     }
   };
   const Magics mg = make_magics<BITS>();
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  f4 acc[NR];
+#pragma unroll
+  for (int rr = 0; rr < NR; ++rr) acc[rr] = f4{0.f, 0.f, 0.f, 0.f};
   uint32_t* slot = &xs[wave][0];
   auto tile = [&](int u) {
     h8 xa[4];
     park_x<MT>(xa, xq[u], slot, lane, n_in);
-    auto step = [&](auto S_) {
-      constexpr int S = decltype(S_)::value;
-      uint32_t v[4];
-      const int si = (u * GPT + S * GPT / 4) * kTileN + n_in;
-      if constexpr (PRE) {
-        dequant_step_pre<BITS, S>(wt[u].pc, mg, sslot[si], sslot[SW + si],
-                                  NPL > 2 ? sslot[(NPL - 1) * SW + si] : 0u, v);
-      } else {
-        const uint32_t szw = SZR ? sslot[si] : wt[u].sz[S * GPT / 4];
-        const GroupQ gq = make_group_w<BITS, ZM>(szw);
-        dequant_step<BITS, ZM, S>(wt[u].pc, mg, gq, v);
-      }
-      const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc, 0, 0, 0);
-    };
-    step(std::integral_constant<int, 0>{});
-    step(std::integral_constant<int, 1>{});
-    step(std::integral_constant<int, 2>{});
-    step(std::integral_constant<int, 3>{});
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      auto step = [&](auto S_) {
+        constexpr int S = decltype(S_)::value;
+        uint32_t v[4];
+        const int si = rr * SWR + (u * GPT + S * GPT / 4) * kTileN + n_in;
+        if constexpr (PRE) {
+          dequant_step_pre<BITS, S>(wt[rr][u].pc, mg, sslot[si], sslot[SW + si],
+                                    NPL > 2 ? sslot[(NPL - 1) * SW + si] : 0u, v);
+        } else {
+          const uint32_t szw = SZR ? sslot[si] : wt[rr][u].sz[S * GPT / 4];
+          const GroupQ gq = make_group_w<BITS, ZM>(szw);
+          dequant_step<BITS, ZM, S>(wt[rr][u].pc, mg, gq, v);
+        }
+        const h8 bb = __builtin_bit_cast(h8, make_uint4(v[0], v[1], v[2], v[3]));
+        acc[rr] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[S], bb, acc[rr], 0, 0, 0);
+      };
+      step(std::integral_constant<int, 0>{});
+      step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{});
+      step(std::integral_constant<int, 3>{});
+    }
   };
   // C row m = 4q + e sits in lane n + 16q, element e: lanes 0..15 hold rows 0..3
-  auto store = [&](int64_t r) {
-    const int64_t b = r / a.Nt;
-    const int64_t row = (r - b * a.Nt) * kTileN + n_in;
-    if (lane < 16 && row < a.N) {
-      const float bv = a.bias ? (float)a.bias[b * a.bs_b + row] : 0.f;
+  auto store = [&](int64_t u) {
 #pragma unroll
-      for (int e = 0; e < MT && e < 4; ++e) {
-        if (e < a.M) {
-          float t = acc[e];
-          if (a.bias) t += bv;
-          a.y[b * a.bs_y + (int64_t)e * a.N + row] = (_Float16)t;
+    for (int rr = 0; rr < NR; ++rr) {
+      const int64_t r = u * NR + rr;
+      const int64_t b = r / a.Nt;
+      const int64_t row = (r - b * a.Nt) * kTileN + n_in;
+      if (lane < 16 && row < a.N) {
+        const float bv = a.bias ? (float)a.bias[b * a.bs_b + row] : 0.f;
+#pragma unroll
+        for (int e = 0; e < MT && e < 4; ++e) {
+          if (e < a.M) {
+            float t = acc[rr][e];
+            if (a.bias) t += bv;
+            a.y[b * a.bs_y + (int64_t)e * a.N + row] = (_Float16)t;
+          }
         }
       }
+      acc[rr] = f4{0.f, 0.f, 0.f, 0.f};
     }
-    acc = f4{0.f, 0.f, 0.f, 0.f};
   };
 
-  // rounds of PF tiles (Kt % PF == 0: a round never straddles two tile rows); every round but
+  // rounds of PFK k-tiles (Kt % PFK == 0: a round never straddles two row units); every round but
   // the last refills each slot right after computing it with the next round's tile
   load_szr(0);
 #pragma unroll
-  for (int u = 0; u < PF; ++u) load(u, u);
-  int64_t cr = r0;  // compute stream: tile row, round start
+  for (int u = 0; u < PFK; ++u) load(u, u);
+  int64_t cr = r0;  // compute stream: row unit, round start
   int ckt = 0;
-  const int64_t rounds = nrows * (a.Kt / PF);
+  const int64_t rounds = nrows * (a.Kt / PFK);
   for (int64_t q = 0; q + 1 < rounds; ++q) {
     park_sz();  // this round's (scale, zero) words into the wave's LDS slot
-    lkt += PF;
+    lkt += PFK;
     if (lkt == a.Kt) {  // wave-uniform
       lkt = 0;
       ++lr;
@@ -239,12 +265,12 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
     }
     load_szr(lkt);
 #pragma unroll
-    for (int u = 0; u < PF; ++u) {
+    for (int u = 0; u < PFK; ++u) {
       tile(u);
       load(u, lkt + u);
     }
-    ckt += PF;
-    if (ckt == a.Kt) {  // wave-uniform: the tile row is complete
+    ckt += PFK;
+    if (ckt == a.Kt) {  // wave-uniform: the row unit is complete
       store(cr);
       ckt = 0;
       ++cr;
@@ -252,35 +278,60 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
   }
   park_sz();
 #pragma unroll
-  for (int u = 0; u < PF; ++u) tile(u);
+  for (int u = 0; u < PFK; ++u) tile(u);
   store(cr);
 }
 
-// resident blocks of a stream-kernel instance per CU (occupancy query, cached per instance)
+// resident blocks of a stream-kernel instance per CU with `dyn` bytes of dynamic LDS (occupancy
+// query, cached per instance)
 template <typename Kern>
-int blocks_per_cu(Kern k) {
+int blocks_per_cu(Kern k, size_t dyn) {
   static const int nb = [&] {
     int n = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * kStreamWaves, 0) ==
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * kStreamWaves, dyn) ==
                        hipSuccess && n > 0
                ? n : 1;
   }();
   return nb;
 }
 
+// The two-row instances fit 5 waves per SIMD in registers, but measured fastest at 4 (lab2_kernel
+// int2 g64 at 5: 127.4 us, at 4: 114.9): their launches pad each block's LDS to a quarter of the
+// CU's 160 KB so that 4 blocks are resident per CU.
+constexpr size_t kCuLds = 160 * 1024;
+template <typename Kern>
+size_t pad_lds_to(Kern k, int blocks_per_cu_wanted) {
+  static const size_t dyn = [&] {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k)) != hipSuccess) return (size_t)0;
+    const size_t want = kCuLds / blocks_per_cu_wanted - 64;
+    return fa.sharedSizeBytes < want ? want - fa.sharedSizeBytes : (size_t)0;
+  }();
+  return dyn;
+}
 
-template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
-int launch_stream_pf(StreamArgs a, hipStream_t st) {
-  auto k = gemv_stream_kernel<BITS, MT, GPT, ZM, PF, SZR>;
+template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR, int NR>
+int launch_stream_nr(StreamArgs a, hipStream_t st) {
+  auto k = gemv_stream_kernel<BITS, MT, GPT, ZM, PF, SZR, NR>;
+  const size_t dyn = NR == 2 ? pad_lds_to(k, 4) : 0;
   // persistent: the grid is the resident capacity (one tile row per wave, a grid of T waves, ran
   // its last round with a third of the loads in flight)
-  const int64_t Wt =
-      std::min<int64_t>(a.T, (int64_t)device_cu_count() * blocks_per_cu(k) * kStreamWaves);
+  const int64_t Wt = std::min<int64_t>(
+      a.T / NR, (int64_t)device_cu_count() * blocks_per_cu(k, dyn) * kStreamWaves);
   a.Wt = Wt;
   const int64_t blocks = (Wt + kStreamWaves - 1) / kStreamWaves;
   a.xcd_chunk = blocks % 8 == 0 ? (int)(blocks / 8) : 0;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * kStreamWaves), 0, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * kStreamWaves), dyn, st, a);
   return (int)hipGetLastError();
+}
+
+// two tile rows per wave for one-row products with narrow zeros and an even tile-row count
+template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR>
+int launch_stream_pf(const StreamArgs& a, hipStream_t st) {
+  if constexpr (MT == 1 && SZR && ZM == kZNarrow && PF == kStreamPF) {
+    if (a.Nt % 2 == 0) return launch_stream_nr<BITS, MT, GPT, ZM, PF, SZR, 2>(a, st);
+  }
+  return launch_stream_nr<BITS, MT, GPT, ZM, PF, SZR, 1>(a, st);
 }
 
 // kStreamPF tiles in flight per wave, 4 when K is not a multiple of 8 tiles (Kt % 4 == 0: host)

@@ -383,7 +383,12 @@ BATCHED_CASES = [(3, 4096, 4096, 4, 128, 1), (4, 777, 768, 3, 64, 2), (2, 300, 3
                  (20, 4112, 512, 4, 128, 1), (20, 4096, 1024, 4, 64, 2),
                  # round-wide (scale, zero) loads: g32 (two 1-KB loads per round), g64 with 4-deep
                  # rounds (lanes wrap over 512 B); group 256 keeps per-tile loads
-                 (3, 528, 1024, 4, 32, 1), (4, 1040, 512, 2, 64, 1), (3, 272, 2048, 3, 256, 2)]
+                 (3, 528, 1024, 4, 32, 1), (4, 1040, 512, 2, 64, 1), (3, 272, 2048, 3, 256, 2),
+                 # two tile rows per wave (M = 1, narrow zeros, even tile-row count): int2 / int3
+                 # g64, int4 g32 (two round loads), int8, a two-row matrix, and more row pairs
+                 # than resident waves with an uneven split
+                 (3, 512, 2048, 2, 64, 1), (2, 288, 1024, 3, 64, 1), (3, 544, 1024, 4, 32, 1),
+                 (4, 4096, 1024, 8, 128, 1), (3, 32, 1024, 4, 128, 1), (20, 4128, 1024, 2, 64, 1)]
 
 
 @pytest.mark.parametrize("case", BATCHED_CASES)

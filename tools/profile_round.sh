@@ -43,6 +43,15 @@ for w in gemv_int3_g64 gemv_int2_g64; do
      --no-decode-layer) || exit $?
   python tools/pmc_traffic.py "$OUT/pmc_$w" gemv_stream ${w}_batched "$OUT/${R}_${w}_batched_pmc.json"
 done
+# the GEMM at configs[2] (M = 65,536): FETCH_SIZE, then the SQ passes (tools/dev/pmc_any.sh)
+(cd /tmp && step pmc_gemm65536 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_gemm" -o run \
+   -- python "$ROOT/bench.py" --workload gemm_int4_g128_m65536 --steps 2 --warmup 1 --no-cpu-baseline) \
+   || exit $?
+python tools/pmc_traffic.py "$OUT/pmc_gemm" gemm_kernel gemm_int4_g128_m65536 \
+  "$OUT/${R}_gemm_int4_g128_m65536_pmc.json"
+step sq_gemm65536 400 bash tools/dev/pmc_any.sh gemm65536 gemm_kernel bench.py \
+  --workload gemm_int4_g128_m65536 --steps 2 --warmup 1 --no-cpu-baseline
+cp "$OUT/sq_gemm65536.out" "$OUT/${R}_gemm_m65536_sq_counters.txt"
 # the decode layer's traffic: every GEMV / attention dispatch of a --no-other-mode run
 (cd /tmp && step pmc_decode 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcd" -o run \
    -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode --ramp-s 0) \
