@@ -285,3 +285,21 @@ def test_generate_graph_replay_matches_eager():
         scale = a.abs().amax(-1)
         rel = ((a - b).abs().amax(-1) / scale)[0]
         assert rel.max().item() <= 5e-3, rel
+
+
+@pytest.mark.gpu
+def test_generate_graphs_fall_back_past_attn_max_l():
+    """A generation whose cache would pass qlin.ATTN_MAX_L rows cannot use the device-length
+    attention (it serves at most that many rows): generate(graphs=True) takes the per-step
+    path instead (PipelineRunner.generate), so its tokens equal the eager path's bit for bit
+    rather than attending over a clamped prefix."""
+    from quant import qlin
+    cfg = _gpu_cfg()
+    cfg.max_position_embeddings = 2 * qlin.ATTN_MAX_L
+    dev = torch.device("cuda", 0)
+    model = _packed_model(cfg, dev)
+    T_ = qlin.ATTN_MAX_L - 2  # prompt + 4 new tokens passes ATTN_MAX_L
+    prompts = [p.to(dev) for p in _prompts(cfg.vocab_size, n=1, B=1, T_=T_)]
+    eager = greedy_generate(model, prompts, 4)
+    graph = greedy_generate(model, prompts, 4, graphs=True)
+    assert torch.equal(eager, graph)

@@ -58,6 +58,15 @@ cp "$OUT/sq_gemm65536.out" "$OUT/${R}_gemm_m65536_sq_counters.txt"
    || exit $?
 python tools/decode_traffic.py "$OUT/pmcd" "$OUT/${R}_decode_layer_int4_g128_pmc.json"
 step decode_layer 300 python tools/bench_decode.py
+# per-launch durations of the graph-replayed decode layers (rocpd database, last 400 dispatches)
+(cd /tmp && step decode_kt 300 rocprofv3 --kernel-trace -d "$OUT/dkt" -o run \
+   -- python "$ROOT/tools/bench_decode.py" --reps 10) || exit $?
+python tools/dev/kstats.py "$(find "$OUT/dkt" -name '*.db' | head -1)" 400 \
+  > "$OUT/${R}_decode_kernel_stats.txt"
 step attn_prefill 300 python tools/dev/attn_prefill_bench.py
 step ppl_llama3_8b 500 python tools/ppl_llama3_8b.py
+# raw profiler outputs stay on the box (gpurun copies back at most 64 MiB): the summaries above
+# are what profiles/ keeps
+rm -rf "$OUT/kt" "$OUT/pmc" "$OUT/pmcl" "$OUT"/pmc_gemv_* "$OUT/pmc_gemm" "$OUT/pmcd" "$OUT/dkt" \
+  "$ROOT/gpurun_out/pmc_gemm65536"
 echo "done: $OUT"
