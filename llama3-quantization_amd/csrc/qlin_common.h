@@ -169,14 +169,20 @@ __device__ __forceinline__ void step_pairs(const Piece<BITS>& c, const Magics& g
     v[2] = (w & 0x00300030u) | g.m64;
     v[3] = (w & 0x00C000C0u) | g.m16;
   } else {
-    // int3: the high bit joins the magic first (pinned, so it is not re-associated), then the
-    // 2-bit field -- two v_and_or_b32 per pair (left to itself the compiler emits AND, AND, OR3)
+    // int3: the (rotated) high-bit word h holds pair P's third bit at bit 2P + 2 of each half,
+    // right above its 2-bit field in w.  Pairs 0 and 2 (fields at bits 0-1, 4-5) and pairs 1 and 3
+    // (2-3, 6-7) each take their fields from w and their high bits from h in ONE bitfield insert
+    // (v_bfi_b32: the bits outside the mask come from h; those no field reads are masked away
+    // below), then one v_and_or_b32 per pair: 6 VALU per k-step instead of 8.  The merged words
+    // are pinned so the masks are not pushed back into AND / AND / OR3.
     const uint32_t w = (S & 1) ? (c.w[S >> 1] >> 8) : c.w[S >> 1];
     const uint32_t h = (rho3(S) == 0) ? c.w[2] : __builtin_amdgcn_alignbit(c.w[2], c.w[2], rho3(S));
-    v[0] = (w & 0x00030003u) | pin_v((h & 0x00040004u) | g.m1024);
-    v[1] = (w & 0x000C000Cu) | pin_v((h & 0x00100010u) | g.m256);
-    v[2] = (w & 0x00300030u) | pin_v((h & 0x00400040u) | g.m64);
-    v[3] = (w & 0x00C000C0u) | pin_v((h & 0x01000100u) | g.m16);
+    const uint32_t w02 = pin_v((w & 0x00330033u) | (h & ~0x00330033u));
+    const uint32_t w13 = pin_v((w & 0x00CC00CCu) | (h & ~0x00CC00CCu));
+    v[0] = (w02 & 0x00070007u) | g.m1024;
+    v[1] = (w13 & 0x001C001Cu) | g.m256;
+    v[2] = (w02 & 0x00700070u) | g.m64;
+    v[3] = (w13 & 0x01C001C0u) | g.m16;
   }
 }
 
