@@ -96,3 +96,23 @@ def test_pack_codes_matches_oracle_packer():
         qw = qlin.pack_codes(t(u), bits)
         ref = O.pack_qweight(u.astype(np.uint32), bits)
         assert np.array_equal(n(qw).view(np.uint32), ref.reshape(n(qw).shape)), bits
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbits,N,K", [(3, 28672, 4096), (2, 4096, 14336)])
+def test_hqq_conversion_llama_widths(nbits, N, K):
+    """configs[3] at LLaMA3-8B widths: an HQQ int3 gate/up-wide matrix (28,672 x 4,096, the
+    work-queue route at one token) and an int2 down-shaped matrix (4,096 x 14,336, the long-K
+    rows route), g64: the converted W_dq is hqq's fp16 ((W_q - zero) * scale) bit for bit, and
+    the decode (M = 1) and a 16-row product match x @ W_dq^T in fp64."""
+    from quant import qlin
+    group = 64
+    W_q, meta, ref_w = _hqq_linear(N, K, nbits, group, seed=nbits * 7 + 1)
+    ql = hqq.packed_quant_linear(W_q, meta)
+    assert ql.qflags & 16
+    assert bit_equal(n(ql.dequantized_weight()), ref_w)
+    assert qlin.m1_route(N, K, nbits, group) in (qlin.M1_WHOLE_ROW, qlin.M1_ROWS)
+    for M in (1, 16):
+        x = rand_x(M, K, seed=M + nbits)
+        y = ql(t(x).unsqueeze(0))[0]
+        assert_close_to_ref(n(y), O.linear_ref(x, ref_w), what=f"hqq int{nbits} {N}x{K} M={M}")
