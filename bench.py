@@ -216,6 +216,11 @@ def decode_layer_bytes(cfg, L, bits=4, group=128):
     return w + 2 * cfg.num_key_value_heads * L * D * 2, sum(2 * N * K for N, K in lin)
 
 
+def graph_steps(n, cap=10):
+    """Steps per captured graph: the largest divisor of n up to cap (n steps = n / G replays)."""
+    return max(g for g in range(1, min(n, cap) + 1) if n % g == 0)
+
+
 def decode_layer_bench(args, dev, timed):
     """The product's decode path (BASELINE configs[1] inside the model): one batch-1 decode step
     through R distinct LLaMA3-8B-shaped QuantLlamaDecoderLayers (hidden 4096, intermediate 14336,
@@ -269,19 +274,24 @@ def decode_layer_bench(args, dev, timed):
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s), torch.no_grad():
         step()
+    # one graph = one 32-layer token's worth of layers (the R distinct layers repeated), as the
+    # decode loop captures a token step: its graph-launch overhead is paid once per token
+    reps = max(1, 32 // R)
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph, stream=s), torch.no_grad():  # capture on the warm-up stream
-        step()
+        for _ in range(reps):
+            step()
     torch.cuda.current_stream(dev).wait_stream(s)
-    steps = max(10, args.steps // 2)
-    el, _ = timed(graph.replay, steps, max(2, args.warmup // 2))
-    us = el / steps / R * 1e6
+    steps = max(5, args.steps // 4)
+    el, _ = timed(graph.replay, steps, max(2, args.warmup // 4))
+    us = el / (steps * reps * R) * 1e6
     nbytes, flops = decode_layer_bytes(cfg, kv + 1)
     out = {"workload": "decode_layer_int4_g128",
            "what": ("LLaMA3-8B decoder layer, batch-1 decode step, int4 g128 packed + fused "
                     "(q/k/v+RMSNorm, attention+RoPE+KV append, o+residual, gate/up+RMSNorm+SiLU*up, "
                     "down+residual: 5 launches), graph-replayed over distinct layers"),
-           "layers": R, "kv_len": kv + 1, "us_per_layer": round(us, 2),
+           "layers": R, "layers_per_graph": reps * R, "kv_len": kv + 1,
+           "us_per_layer": round(us, 2),
            "est_32_layer_token_ms": round(us * 32 / 1e3, 3),
            "tflops": round(flops / us / 1e6, 3),
            "roofline": {"bound": "hbm", "achieved": round(nbytes / us / 1e3, 1),
@@ -289,7 +299,8 @@ def decode_layer_bench(args, dev, timed):
                         "frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
                         "bytes_per_layer": nbytes,
                         "bytes": "7 packed linears by SURVEY §8(d) + the K / V rows read",
-                        "timing": "HIP events over graph replays / layers"}}
+                        "timing": ("HIP events over graph replays / layers (one graph = "
+                                   f"{reps} x the {R} distinct layers)")}}
     pmc = _pmc_traffic("decode_layer_int4_g128")
     if pmc is not None:
         out["roofline"]["traffic"] = round(pmc["fetch_bytes_per_launch"])
@@ -412,7 +423,11 @@ def main():
 
     use_graph = not args.no_graph and kernel in ("gemv", "linear")
 
-    def make_runner(step):
+    def make_runner(step, per_graph=1):
+        """One HIP graph holding `per_graph` consecutive steps (a replay = that many steps): the
+        host's graph-launch overhead (~5 us between the kernels of two replays, against ~0 inside
+        one graph; tools/dev/ring_sweep.py) is paid once per graph, as a serving loop that
+        captures its steps pays it, not once per step."""
         if not use_graph:
             return step
         s = torch.cuda.Stream(dev)
@@ -421,7 +436,8 @@ def main():
             step()  # warm the code objects outside capture
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=s):
-            step()
+            for _ in range(per_graph):
+                step()
         torch.cuda.current_stream(dev).wait_stream(s)
         return graph.replay
 
@@ -458,8 +474,9 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item()), wall_
 
-    elapsed, wall = timed(make_runner(step_batched if batched else step_launches), args.steps,
-                          args.warmup)
+    G = graph_steps(args.steps) if use_graph else 1
+    elapsed, wall = timed(make_runner(step_batched if batched else step_launches, G),
+                          args.steps // G, max(1, -(-args.warmup // G)))
 
     flops = 2.0 * M * N * K
     nbytes = algo_bytes(M, N, K, bits, group)
@@ -495,17 +512,20 @@ def main():
     roof = roofline(per_product_s, R if batched else 1)
     if batched:
         roof["timing"] = ("HIP events over the timed region / launches (one strided-batch launch "
-                          f"of {R} GEMVs per step, graph-replayed)")
+                          f"of {R} GEMVs per step; {G} steps per captured graph)")
     else:
-        roof["timing"] = ("HIP events over the timed region / launches (graph replay of the ring; "
-                          "includes the inter-kernel dispatch gap)" if use_graph else
+        roof["timing"] = ("HIP events over the timed region / launches (graph replay of the ring, "
+                          f"{G} steps per captured graph; includes the inter-kernel dispatch gap)"
+                          if use_graph else
                           "HIP events over the timed region / launches (eager)")
     other = None
     if kernel == "gemv" and not args.no_other_mode:
         # the other mode, timed the same way, reported beside the headline
-        o_el, _ = timed(make_runner(step_launches if batched else step_batched),
-                        max(5, args.steps // 2), max(2, args.warmup // 2))
-        o_per = o_el / (max(5, args.steps // 2) * R)
+        o_steps = max(5, args.steps // 2)
+        oG = graph_steps(o_steps) if use_graph else 1
+        o_el, _ = timed(make_runner(step_launches if batched else step_batched, oG), o_steps // oG,
+                        max(1, -(-max(2, args.warmup // 2) // oG)))
+        o_per = o_el / (o_steps * R)
         other = roofline(o_per, 1 if batched else R)
         other["mode"] = "launches" if batched else "batched"
         other["value"] = round(job_flops / o_per / 1e12, 4)
@@ -527,7 +547,7 @@ def main():
         "hbm_GBps_total": round(nbytes * products * world / elapsed / 1e9, 1),
         "config": {"workload": args.workload, "note": note, "M": M, "N": N_full, "K": K,
                    "N_per_rank": N, "bits": bits, "group_size": group, "ring": R,
-                   "sz_bytes_per_group": 2 + zb, "graph": use_graph,
+                   "sz_bytes_per_group": 2 + zb, "graph": use_graph, "graph_steps": G,
                    "mode": ("batched" if batched else "launches") if kernel == "gemv" else kernel,
                    "parallelism": (f"strong x{world} (output rows split, no collective)"
                                    if args.split else f"weak x{world} (independent rings)")},
