@@ -116,3 +116,29 @@ def test_hqq_conversion_llama_widths(nbits, N, K):
         x = rand_x(M, K, seed=M + nbits)
         y = ql(t(x).unsqueeze(0))[0]
         assert_close_to_ref(n(y), O.linear_ref(x, ref_w), what=f"hqq int{nbits} {N}x{K} M={M}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbits,N", [(3, 512), (2, 528)])
+def test_hqq_batched_bit_identical_to_gemm(nbits, N):
+    """configs[3]'s batched rings with hqq's fp16 zeros (the streaming kernel's float-zero
+    instances; even and odd tile-row counts): every product bit-identical to qlin_gemm_f16 unsplit
+    and close to x @ W_dq^T in fp64."""
+    from quant import qlin
+    K, group, B = 2048, 64, 3
+    convs, refs = [], []
+    for b in range(B):
+        W_q, meta, ref_w = _hqq_linear(N, K, nbits, group, seed=100 * nbits + b)
+        convs.append(hqq.hqq_to_qlin(W_q.cuda(), {k: (v.cuda() if torch.is_tensor(v) else v)
+                                                     for k, v in meta.items()}))
+        refs.append(ref_w)
+    fl = convs[0]["flags"]
+    assert fl & qlin.FLOAT_ZERO
+    qw = torch.stack([c["qweight"] for c in convs])
+    qsz = torch.stack([c["qsz"] for c in convs])
+    x = np.stack([rand_x(1, K, seed=7 + b) for b in range(B)])
+    y = qlin.gemv_batched(t(x), qw, qsz, None, N, K, nbits, group, fl)
+    for b in range(B):
+        yb = qlin.gemm(t(x[b]), qw[b], qsz[b], None, N, K, nbits, group, fl, split=False)
+        assert bit_equal(n(y[b]), n(yb)), f"problem {b}"
+        assert_close_to_ref(n(y[b]), O.linear_ref(x[b], refs[b]), what=f"hqq batched b{nbits} {b}")
