@@ -206,3 +206,15 @@ def test_mask_cache_does_not_keep_masks_alive():
     del m
     gc.collect()
     assert r() is None
+
+
+def test_bench_graph_steps_divide_the_timed_steps():
+    """bench.py captures G steps per graph and replays steps / G graphs: G must divide the step
+    count (the timed region is exactly --steps steps) and stay <= 10."""
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = importlib.import_module("bench")
+    for n, g in ((50, 10), (5, 5), (7, 7), (13, 1), (12, 6), (1, 1), (100, 10)):
+        assert bench.graph_steps(n) == g
+        assert n % bench.graph_steps(n) == 0
