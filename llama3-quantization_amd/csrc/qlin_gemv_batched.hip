@@ -62,10 +62,10 @@ constexpr int kStreamPF = 8;  // tiles in flight per wave (16 for
 // z + off_3) in fp16 (off_P = pair_off<BITS>(P); the sums are exact, |z| <= 1024) -- and a k-step
 // reads its lane's words and subtracts the half its pair needs (op_sel), so the per-pair work is
 // the extract, the zero subtraction and the scale multiply alone: the same fp16 operations on the
-// same values as dequant_step (bit-identical): 62.5 -> 52.4 VALU per int2 g64 tile, 99 -> 73 for
-// int3 with two v_and_or_b32 per pair (step_pairs).  tools/dev/batch_geo.py, one box, best of 3:
-// int2 g64 129.9 -> 126.0 us per 96-matrix ring (119.8 with the int3 build), int3 g64 120.2 ->
-// 108.8 us per 64; int4 g128 +-1 %.
+// same values as dequant_step (bit-identical): 62.5 -> 52.4 VALU per int2 g64 tile (int3: 99 ->
+// 65 with step_pairs' v_bfi_b32 extract).  tools/dev/batch_geo.py, one box, best of 3: int2 g64
+// 129.9 -> 126.0 us per 96-matrix ring, int3 g64 120.2 -> 108.8 us per 64 (the two-v_and_or_b32
+// int3 extract of that build); int4 g128 +-1 %.
 template <int BITS, int S>
 __device__ __forceinline__ void dequant_step_pre(const Piece<BITS>& c, const Magics& mg,
                                                  uint32_t ssw, uint32_t za, uint32_t zb,
