@@ -56,6 +56,9 @@ WORKLOADS = {
 }
 
 
+PIPE_WORKLOAD = "pipeline_llama3_8b_int4_g128"
+
+
 def algo_bytes(M, N, K, bits, group, zero_bytes=1):
     """Algorithmic bytes of one launch, SURVEY.md §8(d) / BASELINE.md §2:
     2MK + N*K*bits/8 + N*(K/g)*(2 + zb) + 2MN with zb = 1 (fp16 scale + int8 zero per group).
@@ -78,12 +81,31 @@ def _pmc_traffic(workload):
     return d
 
 
+def _attach_traffic(roof, pmc, algo):
+    """roofline.traffic from a committed PMC pass, or null: a pass that reports fewer HBM bytes
+    than the launch's algorithmic bytes (every algorithmic byte is read at least once) missed
+    dispatches and is not published; traffic_ratio = traffic / algorithmic."""
+    if pmc is None:
+        return
+    t = pmc["fetch_bytes_per_launch"]
+    roof["traffic_source"] = pmc["file"]
+    if t < algo:
+        roof["traffic"] = None
+        roof["traffic_rejected"] = (f"{pmc['file']}: {round(t)} B < {algo} algorithmic B per "
+                                    "launch (incomplete PMC pass)")
+        return
+    roof["traffic"] = round(t)
+    roof["traffic_ratio"] = round(t / algo, 4)
+
+
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    # default: the launcher's WORLD_SIZE (torchrun without --gpus), else 1
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="gemv_int4_g128", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="gemv_int4_g128",
+                    choices=sorted(WORKLOADS) + [PIPE_WORKLOAD])
     ap.add_argument("--ring", type=int, default=None)
     ap.add_argument("--split", action="store_true",
                     help="strong scaling: every rank streams rows [r*N/P, (r+1)*N/P) of the SAME "
@@ -105,6 +127,18 @@ def parse():
                     help="skip the decode-layer line (configs[1] inside the model, DESIGN.md §5)")
     ap.add_argument("--decode-layers", type=int, default=8)
     ap.add_argument("--decode-kv", type=int, default=512)
+    ap.add_argument("--pipeline", choices=("auto", "on", "off"), default="auto",
+                    help="the configs[4] pipeline leg (32 LLaMA3-8B layers as N stages, RCCL "
+                         "send / recv): auto = with N > 1 ranks or --workload "
+                         f"{PIPE_WORKLOAD}")
+    ap.add_argument("--pipe-layers", type=int, default=32)
+    ap.add_argument("--pipe-tokens", type=int, default=2048, help="tokens per PPL window")
+    ap.add_argument("--pipe-windows", type=int, default=0,
+                    help="windows in flight per timed pass (default: max(4, 2 x ranks))")
+    ap.add_argument("--pipe-decode", type=int, default=16,
+                    help="greedy decode steps per sequence (one sequence per stage), graphs=True")
+    ap.add_argument("--pipe-no-check", action="store_true",
+                    help="skip the one-process reference run (NLL / token bit-identity)")
     return ap.parse_args()
 
 
@@ -301,12 +335,132 @@ def decode_layer_bench(args, dev, timed):
                         "bytes": "7 packed linears by SURVEY §8(d) + the K / V rows read",
                         "timing": ("HIP events over graph replays / layers (one graph = "
                                    f"{reps} x the {R} distinct layers)")}}
-    pmc = _pmc_traffic("decode_layer_int4_g128")
-    if pmc is not None:
-        out["roofline"]["traffic"] = round(pmc["fetch_bytes_per_launch"])
-        out["roofline"]["traffic_source"] = pmc["file"]
+    _attach_traffic(out["roofline"], _pmc_traffic("decode_layer_int4_g128"), nbytes)
     del graph, layers
     torch.cuda.empty_cache()
+    return out
+
+
+def pipeline_bench(args, dev, world, rank, backend):
+    """BASELINE configs[4]: 32 LLaMA3-8B-width decoder layers, RTN int4 g128, packed + fused
+    (prefill-attention kernel for the windows, in-place KV cache for decode), partitioned over the
+    N ranks as contiguous pipeline stages with point-to-point hand-offs of the hidden states (RCCL
+    over xGMI with the nccl backend; models/pipeline.py) — the counterpart of the reference's
+    multi-GPU placement (parallel_utils.py:89-163, main.py:64-80) and PPL loop (main.py:125-151).
+
+      windows: W 2048-token windows in flight through the stages (GPipe fill), Σ NLL per window
+               broadcast from the last stage; ms per window = the max-over-ranks wall time of
+               the whole pass / W.
+      decode:  greedy generation of N sequences (one per stage in flight), every decode step a
+               replayed HIP graph per stage (graphs=True); ms per step = the difference of two
+               runs of different lengths (prefill and captures cancel) / the extra steps.
+      check:   rank 0 builds all layers in one process and runs the same windows and the same
+               generation: NLL and tokens must be bit-identical (each layer sees the same input
+               tensor, only on another device).
+    Random-init weights and synthetic tokens (no checkpoints or datasets offline)."""
+    import torch
+    import torch.distributed as dist
+    from transformers import LlamaConfig
+    from models.pipeline import PipelineRunner, greedy_generate, single_stage_nlls, stage_info
+    from models.quant_llama import build_random_quant_llama, quant_args, rtn_quantize_
+    nl, T = args.pipe_layers, args.pipe_tokens
+    W = args.pipe_windows or max(4, 2 * world)
+    cfg = LlamaConfig(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
+                      num_key_value_heads=8, num_hidden_layers=nl, vocab_size=128256,
+                      max_position_embeddings=max(8192, T + 256), rms_norm_eps=1e-5,
+                      rope_theta=500000.0)
+
+    def build(layer_ids):
+        m = build_random_quant_llama(cfg, quant_args(4, 128), seed=1, device=dev,
+                                     dtype=torch.float16, layer_ids=layer_ids)
+        rtn_quantize_(m, pack=True)
+        for layer in m.layers:
+            layer.fuse_packed_projections(prefill_attention=True, kv_cache=True)
+        return m
+
+    def progress(*a):  # a long leg shows it is alive (stderr; stdout keeps the one JSON line)
+        if rank == 0:
+            print("[pipeline]", *a, file=sys.stderr, flush=True)
+
+    info = stage_info(nl, rank, world)
+    t_b = time.perf_counter()
+    model = build(range(info.lo, info.hi))
+    build_s = time.perf_counter() - t_b
+    progress(f"stage {info.lo}..{info.hi} built in {build_s:.1f}s")
+    g = torch.Generator(device=dev).manual_seed(123)
+    wins = [torch.randint(0, cfg.vocab_size, (1, T), device=dev, generator=g) for _ in range(W)]
+    prompts = [torch.randint(0, cfg.vocab_size, (1, 128), device=dev, generator=g)
+               for _ in range(world)]
+    multi = world > 1
+
+    def wall(fn):
+        torch.cuda.synchronize(dev)
+        if multi:
+            dist.barrier()
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize(dev)
+        if multi:
+            dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
+        if multi:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), r
+
+    runner = PipelineRunner(model, info, (1, T, cfg.hidden_size), torch.float16, dev)
+    first = info.first
+    runner.window_nlls(wins if first else None)  # warm: workspaces, code objects, clocks
+    t_win, nll = wall(lambda: runner.window_nlls(wins if first else None))
+    progress(f"{W} windows: {t_win * 1e3:.1f} ms")
+    dr = PipelineRunner(model, info, (1, 1, cfg.hidden_size), torch.float16, dev)
+    n_long = max(4, args.pipe_decode)
+    n_short = max(2, n_long // 4)
+    wall(lambda: dr.generate(prompts if first else None, 2, graphs=True))  # warm
+    t_s, _ = wall(lambda: dr.generate(prompts if first else None, n_short, graphs=True))
+    t_l, toks = wall(lambda: dr.generate(prompts if first else None, n_long, graphs=True))
+    step_s = (t_l - t_s) / (n_long - n_short)
+    progress(f"decode: {step_s * 1e3:.3f} ms per step")
+    out = {"workload": PIPE_WORKLOAD,
+           "what": (f"{nl} LLaMA3-8B decoder layers (4096 / 14336 / 32q 8kv / vocab 128,256), "
+                    "RTN int4 g128 packed + fused, as contiguous pipeline stages, hidden states "
+                    f"handed stage to stage by {'RCCL (xGMI) ' if backend == 'nccl' else ''}"
+                    f"{backend} send / recv"),
+           "stages": [[stage_info(nl, r, world).lo, stage_info(nl, r, world).hi]
+                      for r in range(world)],
+           "backend": backend, "build_s_rank0": round(build_s, 2),
+           "windows": {"windows_in_flight": W, "tokens_per_window": T,
+                       "ms_per_window": round(t_win / W * 1e3, 3),
+                       "tokens_per_s": round(W * T / t_win, 1),
+                       "ppl": float(torch.exp(nll.double().sum() / (W * T))),
+                       "timing": "wall, barrier + synchronize around one pass, max over ranks"},
+           "decode": {"sequences": world, "prompt": 128, "graphs": True,
+                      "ms_per_step": round(step_s * 1e3, 3),
+                      "ms_per_token_per_sequence": round(step_s * 1e3, 3),
+                      "tokens_per_s": round(world / step_s, 1),
+                      "timing": (f"({n_long} - {n_short}) step difference of two generations, "
+                                 "max over ranks")}}
+    if not args.pipe_no_check:
+        # the one-process reference on rank 0 (every other rank waits at the barrier)
+        ok = torch.zeros(2, dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        if rank == 0:
+            if multi:
+                del runner, dr
+                full = build(range(nl))
+            else:
+                full = model
+            ref_nll = single_stage_nlls(full, wins)
+            progress("one-process reference built")
+            ref_tok = greedy_generate(full, prompts, n_long, graphs=True)
+            ok[0] = int(torch.equal(ref_nll.float(), nll.float().to(ref_nll.device)))
+            ok[1] = int(torch.equal(ref_tok, toks))
+            del full
+            torch.cuda.empty_cache()
+        if multi:
+            dist.broadcast(ok, src=0)
+        out["check"] = {"nll_bit_identical_to_one_process": bool(ok[0]),
+                        "tokens_identical_to_one_process": bool(ok[1]),
+                        "nll": [round(float(v), 6) for v in nll]}
     return out
 
 
@@ -355,6 +509,26 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+
+    if args.workload == PIPE_WORKLOAD:
+        pipe = pipeline_bench(args, dev, world, rank, backend)
+        w = pipe["windows"]
+        out = {"metric": "dequant-matmul TFLOP/s + HBM GB/s, int4 g128 4096x4096; LLaMA3-8B PPL delta",
+               "value": w["tokens_per_s"], "unit": "tokens/s (2048-token PPL windows)",
+               "n_gpus": world, "steps": 1, "warmup": 1,
+               "ms_per_step": w["ms_per_window"] * w["windows_in_flight"],
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "dtype": "f16", "data": "synthetic (random-init weights, random tokens)",
+               "config": {"workload": PIPE_WORKLOAD, "model": "LLaMA3-8B architecture",
+                          "layers": args.pipe_layers, "bits": 4, "group_size": 128,
+                          "parallelism": f"pipeline x{world} (contiguous stages, P2P)"},
+               "pipeline": pipe}
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     M, N_full, K, bits, group, ring, kernel, note = WORKLOADS[args.workload]
     N = N_full
@@ -500,9 +674,7 @@ def main():
         r["traffic"] = None
         pmc_name = args.workload + ("_batched" if launch_products > 1 else "")
         pmc = _pmc_traffic(pmc_name) if not (args.split and world > 1) else None
-        if pmc is not None:
-            r["traffic"] = round(pmc["fetch_bytes_per_launch"])
-            r["traffic_source"] = pmc["file"]
+        _attach_traffic(r, pmc, nbytes * launch_products)
         r["bytes_per_launch"] = nbytes * launch_products
         r["bytes_read_per_launch"] = read_bytes * launch_products
         r["us_per_launch"] = round(per_product * launch_products * 1e6, 3)
@@ -558,6 +730,9 @@ def main():
         out["other_mode"] = other
     if kernel == "gemv" and args.workload == "gemv_int4_g128" and not args.no_decode_layer:
         out["decode_layer"] = decode_layer_bench(args, dev, timed)
+    if args.pipeline == "on" or (args.pipeline == "auto" and world > 1):
+        # configs[4]: the 32-layer pipeline over the same ranks (RCCL P2P between stages)
+        out["pipeline"] = pipeline_bench(args, dev, world, rank, backend)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(M, N, K, bits, group, args.cpu_seconds) \
             if kernel != "gemm" else cpu_baseline(min(M, 32), N, K, bits, group, args.cpu_seconds)

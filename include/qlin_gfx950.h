@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define QLIN_ABI_VERSION 12
+#define QLIN_ABI_VERSION 13
 
 /* quantizer flags (UniformAffineQuantizer options, quant/quantizer.py:24-36) */
 #define QLIN_SYMMETRIC          1
@@ -172,6 +172,18 @@ int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_stride, const
                           const uint16_t* bias, int64_t bias_stride, uint16_t* y,
                           int64_t y_stride, int64_t batch, int64_t M, int64_t N, int64_t K,
                           int bits, int group, void* stream);
+/*
+ * The launch geometry qlin_gemv_batched_f16 uses for these arguments on the current device, without
+ * launching (pointers are only checked for alignment): plan[0] = workgroups of the streaming
+ * kernel, plan[1] = dynamic LDS bytes per workgroup, plan[2] = the instance's static LDS bytes,
+ * plan[3] = resident workgroups per CU (occupancy query of that instance), plan[4] = tile rows per
+ * wave (1 or 2); all 0 when the arguments take the per-problem path.  Introspection for tests and
+ * tools (ABI 13); no reference counterpart.
+ */
+int qlin_gemv_batched_plan(const uint32_t* qweight, int64_t qweight_stride, const uint32_t* qsz,
+                           int64_t qsz_stride, int flags, const uint16_t* x, int64_t x_stride,
+                           int64_t batch, int64_t M, int64_t N, int64_t K, int bits, int group,
+                           int64_t* plan);
 int qlin_linear_f16(const uint32_t* qweight, const uint32_t* qsz, int flags, const uint16_t* x,
                     const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K, int bits,
                     int group, void* stream);
@@ -191,8 +203,9 @@ int qlin_gemm_block_cols(int64_t M, int64_t N, int bits);
 
 /*
  * Which kernel a one-token-row product (qlin_gemv_f16 / qlin_linear_ep_f16 at M = 1, 16-B aligned
- * x, and qlin_rmsnorm_linear_ep_f16) of this shape runs on the current device: 1 = the whole-row
- * kernel (wide matrices), 2 = the fast split-K kernel, 3 = the rows kernel (long K), 0 = the
+ * x, and qlin_rmsnorm_linear_ep_f16) of this shape runs on the current device: 1 = the work-queue
+ * kernel (wide matrices: each CU's workgroup takes chunks of 4 k-tiles of its tile rows from an LDS
+ * counter and adds the chunks' partial sums per row in k order), 2 = the fast split-K kernel, 3 = the rows kernel (long K), 0 = the
  * general GEMV kernel (no M = 1 route: qlin_rmsnorm_linear_ep_f16 rejects the shape), -1 =
  * invalid arguments.  Introspection for tests and tools (ABI 12); no reference counterpart.
  */

@@ -8,15 +8,17 @@
 // five times; this kernel streams K / V once per query block and keeps the scores on chip
 // (online softmax).
 //
-// Arithmetic: the fp32 operands (q, the probabilities P) enter the fp16 matrix cores as unevaluated
-// fp16 pairs x = hi + lo (|x - hi - lo| <= 2^-22 |x|; P scaled by 2^12 first so small
-// probabilities keep their pair out of the subnormals), K / V are fp16 exactly, every product is
-// exact and v_mfma_f32_16x16x32_f16 accumulates in fp32 — the reference's fp32 matmuls to within
-// a few fp32 ulps, at 8x the rate of the fp32 matrix instructions (two fp16 MFMAs per product
-// block).  The scores get the reference's scaling (x the fp32 reciprocal of sqrt(d), as torch
-// divides by a scalar), additive mask and clamp; the softmax is the online form (running max m,
-// sum l, output rescaled by exp(m_old - m_new)).  Results agree with the reference to fp32
-// rounding (summation order, exp(a) exp(b) vs exp(a + b)), not bit for bit.
+// Arithmetic, in the reference's order (round 6): the fp32 operands (q, the
+// probabilities P) enter the fp16 matrix cores as unevaluated sums of THREE fp16 terms (exact:
+// 33 significand bits for fp32's 24), K / V are fp16 exactly, every product is exact and
+// v_mfma_f32_16x16x32_f16 accumulates in fp32 — the reference's fp32 matmuls up to summation
+// order.  The scores are formed as the reference forms them — (q . k) x fp32(1 / sqrt(d)) (torch
+// divides by a scalar as a multiplication by the fp32 reciprocal), + mask, max(., finfo.min) — and
+// the softmax takes two passes over the keys: pass 1 the exact row maximum m, pass 2
+// p = expf(s - m) (libm expf, as torch's softmax kernel), l = sum p and O = sum p v; out = O / l.
+// So no running maximum, no rescaling and no exp2 change of base: each p is the reference's own
+// value whenever the score is, and what remains is fp32 summation order (of q . k, l and p v)
+// and O / l against sum (p / l) v.
 //
 // Decomposition: a 256-thread block = 4 waves = (hw query heads of one KV head) x (4 / hw 16-row
 // query sub-blocks), hw = min(Hq / Hkv, 4), so each staged K / V block serves hw heads (GQA: K / V
@@ -28,7 +30,8 @@
 // fragments of two sub-blocks are, as they stand, the P^T operand of O^T = V^T P^T for a 32-key
 // step whose keys run in the order 4 j + e, 16 + 4 j + e; V^T comes from the row-major V tile by
 // ds_read_b64_tr_b16 (hardware transpose read) in that same key order (32 MFMAs).  The next
-// block's K / V rows and mask values are fetched into registers while a block computes.
+// block's K / V rows and mask values are fetched into registers while a block computes.  Pass 1
+// stages only K.
 //
 // Causal windows (mask verified causal on the host): key blocks past a query block's last
 // diagonal position are skipped — their mask entries are <= -1e4, so exp() underflows to exactly
@@ -45,10 +48,6 @@ namespace {
 constexpr int kD = 128;       // head_dim
 constexpr int kKB = 64;       // keys per block
 constexpr int kMaxG = 8;      // query heads per KV head
-constexpr float kLog2e = 1.4426950408889634f;
-// the reference point moves when the row max passes it by this (exp2 units: p 2^12 < 2^15;
-// 0 = rescale on every new maximum, measured slower in round 3)
-constexpr float kLazy = 3.f;
 
 struct PrefillArgs {
   const float* q;      // [B, Hq, S, D]
@@ -80,12 +79,15 @@ __device__ __forceinline__ float row16_max(float v) {
   return v;
 }
 
-// fp32 value as an unevaluated pair of fp16 (hi = RN16(x), lo = RN16(x - hi)): |x - hi - lo| <=
-// 2^-22 |x| in the normal range
-__device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
+// fp32 value as an unevaluated sum of three fp16 (hi = RN16(x), mid = RN16(x - hi), lo =
+// RN16(x - hi - mid); each difference is exact in fp32): 33 significand bits hold x's 24, so
+// hi + mid + lo == x whenever the terms stay normal
+__device__ __forceinline__ void split3(float x, _Float16& hi, _Float16& mid, _Float16& lo) {
 #pragma clang fp contract(off)
   hi = (_Float16)x;
-  lo = (_Float16)(x - (float)hi);
+  const float r = x - (float)hi;
+  mid = (_Float16)r;
+  lo = (_Float16)(r - (float)mid);
 }
 
 typedef __fp16 tr4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
@@ -110,12 +112,6 @@ __device__ __forceinline__ float groups_max(float v) {
   return fmaxf(x, y);
 }
 __device__ __forceinline__ float groups_sum(float v) { return qlin::cols4_sum(v); }
-
-// p 2^12 as an unevaluated fp16 pair (the scaling is exact; hi + lo within 2^-22 relative)
-__device__ __forceinline__ void split_p(float p, _Float16& hi, _Float16& lo) {
-  hi = (_Float16)(p * 4096.f);
-  lo = (_Float16)__builtin_fmaf(p, 4096.f, -(float)hi);  // exact in fp32, one fp16 rounding
-}
 
 // GMASK: the mask values are read (any mask but the pure causal pattern)
 // K / V tiles in LDS: [64 keys][256 B] unpadded, 16-B chunk c of key row r stored at chunk
@@ -175,13 +171,14 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   }
   const int nkb = (kend + kKB - 1) / kKB;
 
-  // q as fp16 pairs, the B operand of S^T = K Q^T: lane (n, j), d-step t holds
-  // q[row0 + n][32 t + 8 j .. + 7], scaled by 2^8 (taken back exactly from every score) so the lo
-  // halves of small elements stay out of the fp16 subnormals.  Only a power of two: q pre-scaled
-  // by log2(e) / sqrt(d) (scores straight in exp2 units) measured 1e-5 relative output errors
-  // against 3e-7 (tools/dev/ap_num.py).
+  // q as THREE fp16 terms (the B operand of S^T = K Q^T): lane (n, j), d-step t holds
+  // q[row0 + n][32 t + 8 j .. + 7] x 2^8 = hi + mid + lo, each the fp16 rounding of what the
+  // previous terms leave (the differences are exact in fp32): 33 significand bits cover q's 24,
+  // so every product k q_term is exact and the fp32 MFMA accumulation is the only rounding — the
+  // reference's fp32 bmm up to summation order.  The 2^8 (taken back exactly from every score)
+  // keeps the low terms of small elements out of the fp16 subnormals.
   const float qscale = 256.f;
-  qlin::h8 qh[4], ql[4];
+  qlin::h8 qh[4], qm[4], ql[4];
   {
     const float* qp = a.q + (((int64_t)b * a.Hq + hq) * S + min(row, S - 1)) * kD + 8 * j;
 #pragma unroll
@@ -190,22 +187,15 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
       const f4v x1 = reinterpret_cast<const f4v*>(qp + 32 * t)[1];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        _Float16 h, l;
-        split16((e < 4 ? x0[e] : x1[e - 4]) * qscale, h, l);
+        _Float16 h, md, lo;
+        split3((e < 4 ? x0[e] : x1[e - 4]) * qscale, h, md, lo);
         qh[t][e] = h;
-        ql[t][e] = l;
+        qm[t][e] = md;
+        ql[t][e] = lo;
       }
     }
   }
-  // O^T accumulators: lane (n, j), d block c holds O[row][16 c + 4 j + e]
-  f4v o[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) o[c] = f4v{0.f, 0.f, 0.f, 0.f};
-  // running reference point m (exp2 units) of the lane's row and sum l of exp2(t - m) over the
-  // lane's keys of it
   const float sinv = a.inv * (1.f / 256.f);  // exact: 1 / 256 is a power of two
-  const float tinv = sinv * kLog2e;
-  float m = -INFINITY, l = 0.f;
 
   const _Float16* kbase = a.k + ((int64_t)b * a.Hkv + hkv) * L * kD;
   const _Float16* vbase = a.v + ((int64_t)b * a.Hkv + hkv) * L * kD;
@@ -229,14 +219,15 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
     dvo[i] = (uint32_t)(r * (kD * 2) + 16 * ((lane & 15) ^ swz(r)));
   }
   float mk[4][4];  // GMASK: the next block's mask values of the lane
-  auto fetch = [&](int stage, int k0) {
+  auto fetch = [&](int stage, int k0, bool with_v) {
     unsigned char* kd = &kvs[stage][0][0] + wave * 4096;
     unsigned char* vd = &kvs[stage][1][0] + wave * 4096;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const uint32_t vo = dvo[i] + (uint32_t)k0 * (kD * 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_ptr)(kd + 1024 * i), 16, vo, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_ptr)(vd + 1024 * i), 16, vo, 0, 0, 0);
+      if (with_v)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_ptr)(vd + 1024 * i), 16, vo, 0, 0, 0);
     }
     if constexpr (GMASK) {
 #pragma unroll
@@ -254,8 +245,56 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
   const int fk = swz(n);
   const int vrow = 4 * j + (n >> 2);
   const int fv = swz(vrow);
-  fetch(0, 0);
 
+  // The reference's scores of key block k0 for the lane's row, in the reference's order:
+  // s = (q . k) (fp32 matmul) x fp32(1 / sqrt(d)) (torch divides by a scalar as a multiplication
+  // by the fp32 reciprocal), + mask (fp32 add of the mask value), then max(., finfo(fp32).min) —
+  // models/int_llama_layer.py:143-157.  Keys past L and, in the pure causal pattern, keys past the
+  // row's diagonal drop out as -inf (the reference's exp() of a masked score is exactly 0 too).
+  // Both passes evaluate this identically, so pass 2 sees the very values pass 1 took the max of.
+  auto scores = [&](const unsigned char* ks, const float (&mc)[4][4], int k0, f4v (&sc)[4]) {
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) sc[sb] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int sb = 0; sb < 4; ++sb) {
+        const qlin::h8 kf = *reinterpret_cast<const qlin::h8*>(
+            ks + (16 * sb + n) * (kD * 2) + 16 * ((4 * t + j) ^ fk));
+        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[t], sc[sb], 0, 0, 0);
+        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qm[t], sc[sb], 0, 0, 0);
+        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[t], sc[sb], 0, 0, 0);
+      }
+    auto finish = [&](auto CHK_) {
+      constexpr bool CHK = decltype(CHK_)::value;
+#pragma unroll
+      for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma clang fp contract(off)
+          float sv = sc[sb][e] * sinv;
+          if constexpr (GMASK) {
+            sv = sv + mc[sb][e];
+            sv = (sv != sv) ? sv : fmaxf(sv, -3.402823466e38f);
+          }
+          if constexpr (CHK) {
+            const int kk = k0 + 16 * sb + 4 * j + e;
+            const bool open = kk < L && (a.causal != 2 || kk <= off + row);
+            sv = open ? sv : -INFINITY;
+          }
+          sc[sb][e] = sv;
+        }
+    };
+    // per-key checks only on blocks that reach past L or (pure causal pattern) past a diagonal
+    if (k0 + kKB > L || (a.causal == 2 && k0 + kKB - 1 > off + row0))  // wave-uniform
+      finish(std::true_type{});
+    else
+      finish(std::false_type{});
+  };
+
+  // ---- pass 1: the exact row maximum m of the scores (K blocks only) ----
+  float m = -INFINITY;
+  fetch(0, 0, false);
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * kKB;
     // block kb has landed for every wave (each drains its own DMA), and every wave is done with
@@ -269,95 +308,64 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
 #pragma unroll
         for (int e = 0; e < 4; ++e) mc[sb][e] = mk[sb][e];
     }
-    if (kb + 1 < nkb) fetch((kb + 1) & 1, k0 + kKB);  // lands while this block computes
+    // the last pass-1 block prefetches pass 2's first (K and V)
+    if (kb + 1 < nkb) fetch((kb + 1) & 1, k0 + kKB, false);
+    else fetch((kb + 1) & 1, 0, true);
     if (!wave_rows || k0 >= kend_w) continue;  // wave-uniform; the wave still stages and syncs
-    const unsigned char* ks = &kvs[kb & 1][0][0];
-    const unsigned char* vs = &kvs[kb & 1][1][0];
-
-    // S^T = K Q^T (fp32 accumulate of k q_hi + k q_lo): lane (n, j) of sub-block sb holds
-    // S[row][k0 + 16 sb + 4 j + e]
     f4v sc[4];
+    scores(&kvs[kb & 1][0][0], mc, k0, sc);
 #pragma unroll
-    for (int sb = 0; sb < 4; ++sb) sc[sb] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int e = 0; e < 4; ++e) m = fmaxf(m, sc[sb][e]);
+  }
+  m = groups_max(m);
+
+  // ---- pass 2: p = exp(s - m) (torch's softmax exponent, libm expf), l = sum p, O = sum p v ----
+  // O^T accumulators (x 2^15): lane (n, j), d block c holds O[row][16 c + 4 j + e]
+  f4v o[8];
 #pragma unroll
-      for (int sb = 0; sb < 4; ++sb) {
-        const qlin::h8 kf = *reinterpret_cast<const qlin::h8*>(
-            ks + (16 * sb + n) * (kD * 2) + 16 * ((4 * t + j) ^ fk));
-        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[t], sc[sb], 0, 0, 0);
-        sc[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[t], sc[sb], 0, 0, 0);
-      }
-    // scores in exp2 units t = s log2(e): s = the reference's x 1 / sqrt(d) (x the fp32
-    // reciprocal, as torch divides by a scalar; the 2^-8 is exact), with a mask + mask and the
-    // clamp at finfo(fp32).min (clamped again after x log2(e), so a fully masked row stays
-    // uniform as in the reference); without a mask one multiply by log2(e) / (256 sqrt(d)).  Keys
-    // past L, and in the pure causal pattern keys past the row's diagonal, drop out (-inf: exp2
-    // gives the reference's exact 0)
-    float mloc = -INFINITY;
-    auto finish_scores = [&](auto CHK_) {
-      constexpr bool CHK = decltype(CHK_)::value;
+  for (int c = 0; c < 8; ++c) o[c] = f4v{0.f, 0.f, 0.f, 0.f};
+  float l = 0.f;  // the lane's keys of its row; summed over the row's lane groups at the end
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * kKB;
+    const int st = (nkb + kb) & 1;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    float mc[4][4];
+    if constexpr (GMASK) {
 #pragma unroll
       for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-#pragma clang fp contract(off)
-          float sv;
-          if constexpr (GMASK) {
-            sv = sc[sb][e] * sinv + mc[sb][e];
-            sv = (sv != sv) ? sv
-                            : fmaxf(fmaxf(sv, -3.402823466e38f) * kLog2e, -3.402823466e38f);
-          } else {
-            sv = sc[sb][e] * tinv;
-          }
-          if constexpr (CHK) {
-            const int kk = k0 + 16 * sb + 4 * j + e;
-            const bool open = kk < L && (a.causal != 2 || kk <= off + row);
-            sv = open ? sv : -INFINITY;
-          }
-          sc[sb][e] = sv;
-          mloc = fmaxf(mloc, sv);
-        }
-    };
-    // per-key checks only on blocks that reach past L or (pure causal pattern) past a diagonal
-    if (k0 + kKB > L || (a.causal == 2 && k0 + kKB - 1 > off + row0))  // wave-uniform
-      finish_scores(std::true_type{});
-    else
-      finish_scores(std::false_type{});
-    // online softmax over the row's 64 keys (its 16 values on this lane, x 4 lane groups); the
-    // reference point m moves only when the row maximum passes it by more than 3 (lazy rescale:
-    // p 2^12 stays below 2^15, inside fp16, and the O / l rescale of every key block is skipped
-    // once the maxima settle); l is kept per lane (the lane's keys) and summed over the row's
-    // lane groups once, at the end
-    mloc = groups_max(mloc);
-    const float mn = fmaxf(m, mloc);
-    if (__builtin_amdgcn_ballot_w64(mn > m + kLazy)) {  // wave-uniform branch
-      const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mn);
-      m = mn;
-      l *= alpha;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) o[c] *= alpha;
+        for (int e = 0; e < 4; ++e) mc[sb][e] = mk[sb][e];
     }
-    const float mref = (m == -INFINITY) ? 0.f : m;
+    if (kb + 1 < nkb) fetch(st ^ 1, k0 + kKB, true);  // lands while this block computes
+    if (!wave_rows || k0 >= kend_w) continue;
+    const unsigned char* vs = &kvs[st][1][0];
+    f4v sc[4];
+    scores(&kvs[st][0][0], mc, k0, sc);
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = __builtin_amdgcn_exp2f(sc[sb][e] - mref);
+#pragma clang fp contract(off)
+        const float pv = expf(sc[sb][e] - m);
         sc[sb][e] = pv;
         l += pv;
       }
     // O^T += V^T P^T: key step t (32 keys) in slot order 32 t + 4 j + e, then 32 t + 16 + 4 j + e —
-    // P^T is the S^T fragments of sub-blocks 2t, 2t + 1 as they stand; V^T by transposed reads of
-    // the row-major V tile (lane 4 q + p of group j: key 32 t [+ 16] + 4 j + q, d 16 c + 4 p)
+    // P^T is the S^T fragments of sub-blocks 2t, 2t + 1 as they stand (p 2^15 as three fp16
+    // terms: exact, p <= 1 against the exact row max); V^T by transposed reads of the row-major V
+    // tile (lane 4 q + p of group j: key 32 t [+ 16] + 4 j + q, d 16 c + 4 p)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      qlin::h8 ph, pl;
+      qlin::h8 ph, pm, pl;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        _Float16 h, lo;
-        split_p(sc[2 * t + (e >> 2)][e & 3], h, lo);
+        _Float16 h, md, lo;
+        split3(sc[2 * t + (e >> 2)][e & 3] * 32768.f, h, md, lo);
         ph[e] = h;
+        pm[e] = md;
         pl[e] = lo;
       }
       const unsigned char* vr0 = vs + (32 * t + vrow) * (kD * 2) + 8 * (n & 1);
@@ -368,6 +376,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
         const uint2 hi4 = tr_read(reinterpret_cast<const _Float16*>(vr0 + 16 * (kD * 2) + 16 * ch));
         const qlin::h8 vf = __builtin_bit_cast(qlin::h8, make_uint4(lo4.x, lo4.y, hi4.x, hi4.y));
         o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, ph, o[c], 0, 0, 0);
+        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pm, o[c], 0, 0, 0);
         o[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pl, o[c], 0, 0, 0);
       }
     }
@@ -375,8 +384,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const PrefillArgs a) 
 
   if (!wave_rows || row >= S) return;
   // O / l -> out[b][row][hq][16 c + 4 j .. + 3] (the layer's transpose(1, 2) layout; fp16 = its
-  // .to(fp16))
-  const float rl = groups_sum(l) * 4096.f;
+  // .to(fp16)); the 2^15 comes back exactly with l
+  const float rl = groups_sum(l) * 32768.f;
   const int64_t base = (((int64_t)b * S + row) * a.Hq + hq) * kD + 4 * j;
 #pragma unroll
   for (int c = 0; c < 8; ++c) {

@@ -44,6 +44,8 @@ struct StreamArgs {
   int64_t Wt;        // waves of the launch (<= T); wave w streams tile rows [wT/Wt, (w+1)T/Wt)
   uint32_t cmagic;   // GPT == 1: kt / (group / 128) = (kt * cmagic) >> 31
   int xcd_chunk;     // > 0: blocks per XCD of the remapped order (grid % 8 == 0)
+  int64_t* plan;     // host only: non-NULL = report {blocks, dyn LDS, static LDS, blocks per CU}
+                     // of the launch into plan[0..3] instead of launching (qlin_gemv_batched_plan)
 };
 
 constexpr int kStreamWaves = 4;
@@ -282,46 +284,67 @@ __global__ __launch_bounds__(64 * kStreamWaves) void gemv_stream_kernel(const St
   store(cr);
 }
 
-// resident blocks of a stream-kernel instance per CU with `dyn` bytes of dynamic LDS (occupancy
-// query, cached per instance)
+// resident blocks per CU of a stream-kernel instance with `dyn` bytes of dynamic LDS (occupancy
+// query; the caller caches it per instance)
 template <typename Kern>
 int blocks_per_cu(Kern k, size_t dyn) {
-  static const int nb = [&] {
-    int n = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * kStreamWaves, dyn) ==
-                       hipSuccess && n > 0
-               ? n : 1;
-  }();
-  return nb;
+  int n = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64 * kStreamWaves, dyn) ==
+                     hipSuccess && n > 0
+             ? n : 1;
+}
+
+template <typename Kern>
+size_t static_lds(Kern k) {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k)) == hipSuccess
+             ? fa.sharedSizeBytes : 0;
 }
 
 // The two-row instances fit 5 waves per SIMD in registers, but measured fastest at 4 (lab2_kernel
 // int2 g64 at 5: 127.4 us, at 4: 114.9): their launches pad each block's LDS to a quarter of the
-// CU's 160 KB so that 4 blocks are resident per CU.
+// CU's 160 KB so that 4 blocks are resident per CU.  Each instance has its own static LDS size,
+// so the padding is computed from that instance's own sharedSizeBytes.
 constexpr size_t kCuLds = 160 * 1024;
-template <typename Kern>
-size_t pad_lds_to(Kern k, int blocks_per_cu_wanted) {
-  static const size_t dyn = [&] {
-    hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k)) != hipSuccess) return (size_t)0;
-    const size_t want = kCuLds / blocks_per_cu_wanted - 64;
-    return fa.sharedSizeBytes < want ? want - fa.sharedSizeBytes : (size_t)0;
-  }();
-  return dyn;
+inline size_t pad_lds_to(size_t static_bytes, int blocks_per_cu_wanted) {
+  const size_t want = kCuLds / blocks_per_cu_wanted - 64;
+  return static_bytes < want ? want - static_bytes : (size_t)0;
 }
+
+// Geometry of one stream-kernel instance, computed once per template instance (a function-local
+// static of the instance's own launcher: every gemv_stream_kernel<...> has the same C++ type, so
+// a cache keyed on the kernel's type would be shared by all of them).
+struct StreamGeo {
+  size_t dyn, stat;
+  int per_cu;
+};
 
 template <int BITS, int MT, int GPT, int ZM, int PF, bool SZR, int NR>
 int launch_stream_nr(StreamArgs a, hipStream_t st) {
   auto k = gemv_stream_kernel<BITS, MT, GPT, ZM, PF, SZR, NR>;
-  const size_t dyn = NR == 2 ? pad_lds_to(k, 4) : 0;
+  static const StreamGeo geo = [&] {
+    StreamGeo g;
+    g.stat = static_lds(k);
+    g.dyn = NR == 2 ? pad_lds_to(g.stat, 4) : 0;
+    g.per_cu = blocks_per_cu(k, g.dyn);
+    return g;
+  }();
   // persistent: the grid is the resident capacity (one tile row per wave, a grid of T waves, ran
   // its last round with a third of the loads in flight)
   const int64_t Wt = std::min<int64_t>(
-      a.T / NR, (int64_t)device_cu_count() * blocks_per_cu(k, dyn) * kStreamWaves);
+      a.T / NR, (int64_t)device_cu_count() * geo.per_cu * kStreamWaves);
   a.Wt = Wt;
   const int64_t blocks = (Wt + kStreamWaves - 1) / kStreamWaves;
+  if (a.plan) {
+    a.plan[0] = blocks;
+    a.plan[1] = (int64_t)geo.dyn;
+    a.plan[2] = (int64_t)geo.stat;
+    a.plan[3] = geo.per_cu;
+    a.plan[4] = NR;
+    return 0;
+  }
   a.xcd_chunk = blocks % 8 == 0 ? (int)(blocks / 8) : 0;
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * kStreamWaves), dyn, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * kStreamWaves), geo.dyn, st, a);
   return (int)hipGetLastError();
 }
 
@@ -355,12 +378,12 @@ int launch_stream_t(const StreamArgs& a, hipStream_t st) {
 // (grid Nt x batch): the per-launch floor of a dependent 4096^2 GEMV (kernel boundary + wave ramp,
 // DESIGN.md §4) is paid once per batch instead of once per matrix.  Problems the decode fast path
 // does not take (M > 4, K % 128, tiles per wave > 4) run as one gemv launch each.
-extern "C" int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_stride,
-                                     const uint32_t* qsz, int64_t qsz_stride, int flags,
-                                     const uint16_t* x, int64_t x_stride, const uint16_t* bias,
-                                     int64_t bias_stride, uint16_t* y, int64_t y_stride,
-                                     int64_t batch, int64_t M, int64_t N, int64_t K, int bits,
-                                     int group, void* stream) {
+namespace {
+int gemv_batched(const uint32_t* qweight, int64_t qweight_stride, const uint32_t* qsz,
+                 int64_t qsz_stride, int flags, const uint16_t* x, int64_t x_stride,
+                 const uint16_t* bias, int64_t bias_stride, uint16_t* y, int64_t y_stride,
+                 int64_t batch, int64_t M, int64_t N, int64_t K, int bits, int group,
+                 void* stream, int64_t* plan) {
   if (!qweight || !qsz || !x || !y || batch < 0 || batch > 65535 || M < 1 || M > kGemvMaxM ||
       !valid_layout(N, K, bits, group))
     return QLIN_EINVAL;
@@ -392,6 +415,8 @@ extern "C" int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_st
     a.T = Nt * batch;
     const uint64_t c = group % kTileK == 0 ? (uint64_t)(group / kTileK) : 1;
     a.cmagic = (uint32_t)(((1ull << 31) + c - 1) / c);
+    a.xcd_chunk = 0;
+    a.plan = plan;
     const int zm = zero_mode(flags), m = (int)M;
 #define QLIN_SM(B, Z, G)                                                                       \
   return m == 1 ? launch_stream_t<B, 1, G, Z>(a, st)                                   \
@@ -416,6 +441,10 @@ extern "C" int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_st
 #undef QLIN_SM
   }
   // anything else: one launch per problem
+  if (plan) {
+    plan[0] = plan[1] = plan[2] = plan[3] = plan[4] = 0;  // not the streaming kernel
+    return QLIN_OK;
+  }
   for (int64_t b = 0; b < batch; ++b) {
     const int rc = qlin::gemv_ep(qweight + b * qweight_stride, qsz + b * qsz_stride, flags,
                                  x + b * x_stride, bias ? bias + b * bias_stride : nullptr,
@@ -424,4 +453,30 @@ extern "C" int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_st
     if (rc) return rc;
   }
   return QLIN_OK;
+}
+
+}  // namespace
+
+extern "C" int qlin_gemv_batched_f16(const uint32_t* qweight, int64_t qweight_stride,
+                                     const uint32_t* qsz, int64_t qsz_stride, int flags,
+                                     const uint16_t* x, int64_t x_stride, const uint16_t* bias,
+                                     int64_t bias_stride, uint16_t* y, int64_t y_stride,
+                                     int64_t batch, int64_t M, int64_t N, int64_t K, int bits,
+                                     int group, void* stream) {
+  return gemv_batched(qweight, qweight_stride, qsz, qsz_stride, flags, x, x_stride, bias,
+                      bias_stride, y, y_stride, batch, M, N, K, bits, group, stream, nullptr);
+}
+
+// The launch geometry qlin_gemv_batched_f16 would use for these arguments (nothing launched);
+// operands are checked for alignment only, never dereferenced.
+extern "C" int qlin_gemv_batched_plan(const uint32_t* qweight, int64_t qweight_stride,
+                                      const uint32_t* qsz, int64_t qsz_stride, int flags,
+                                      const uint16_t* x, int64_t x_stride, int64_t batch,
+                                      int64_t M, int64_t N, int64_t K, int bits, int group,
+                                      int64_t* plan) {
+  if (!plan) return QLIN_EINVAL;
+  for (int i = 0; i < 5; ++i) plan[i] = 0;
+  uint16_t* y_dummy = reinterpret_cast<uint16_t*>(16);
+  return gemv_batched(qweight, qweight_stride, qsz, qsz_stride, flags, x, x_stride, nullptr, 0,
+                      y_dummy, M * N, batch, M, N, K, bits, group, nullptr, plan);
 }

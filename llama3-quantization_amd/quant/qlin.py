@@ -18,7 +18,7 @@ import torch
 LIB_NAME = "libqlin_gfx950.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
                         LIB_NAME)
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 SYMMETRIC = 1
 DISABLE_ZERO_POINT = 2
@@ -50,6 +50,7 @@ SIGNATURES = {
     "qlin_gemm_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p, _l, _p], _i),
     "qlin_gemv_batched_f16": ([_p, _l, _p, _l, _i, _p, _l, _p, _l, _p, _l, _l, _l, _l, _l, _i, _i,
                                _p], _i),
+    "qlin_gemv_batched_plan": ([_p, _l, _p, _l, _i, _p, _l, _l, _l, _l, _l, _i, _i, _p], _i),
     "qlin_linear_f16": ([_p, _p, _i, _p, _p, _p, _l, _l, _l, _i, _i, _p], _i),
     "qlin_gemm_block_cols": ([_l, _l, _i], _i),
     "qlin_gemv_m1_route": ([_l, _l, _i, _i], _i),
@@ -357,6 +358,22 @@ def gemv_batched(x, qweight, qsz, bias, N, K, bits, group, flags=0, out=None):
     return y
 
 
+def gemv_batched_plan(x, qweight, qsz, N, K, bits, group, flags=0):
+    """The launch geometry ``gemv_batched`` would use for these operands (nothing launched;
+    ``qlin_gemv_batched_plan``): dict(blocks, dyn_lds, static_lds, blocks_per_cu, rows_per_wave),
+    all 0 when the arguments take the per-problem path."""
+    B = qweight.shape[0]
+    shared_x = x.dim() == 2
+    M = x.shape[0] if shared_x else x.shape[1]
+    plan = (ctypes.c_int64 * 5)()
+    rc = load_library().qlin_gemv_batched_plan(
+        _ptr(qweight), qweight[0].numel(), _ptr(qsz), qsz[0].numel(), flags, _ptr(x),
+        0 if shared_x else M * K, B, M, N, K, bits, group, plan)
+    _check(rc, "qlin_gemv_batched_plan")
+    return dict(zip(("blocks", "dyn_lds", "static_lds", "blocks_per_cu", "rows_per_wave"),
+                    list(plan)))
+
+
 def gemm(x, qweight, qsz, bias, N, K, bits, group, flags=0, split=True):
     """``qlin_gemm_f16``; ``split``: pass the split-K workspace (small grids split K)."""
     M = x.numel() // K if K else 0
@@ -414,12 +431,14 @@ def linear_ep(x, qweight, qsz, bias, N, K, bits, group, flags=0, epilogue=EP_NON
     return y
 
 
-M1_GENERAL, M1_WHOLE_ROW, M1_FAST, M1_ROWS = 0, 1, 2, 3
+M1_GENERAL, M1_WORK_QUEUE, M1_FAST, M1_ROWS = 0, 1, 2, 3
+M1_WHOLE_ROW = M1_WORK_QUEUE  # round-4 name of route 1 (its whole-row kernel became the work queue)
 
 
 def m1_route(N, K, bits, group):
     """The kernel a one-token-row product of this shape runs (``qlin_gemv_m1_route``):
-    M1_WHOLE_ROW (wide matrices), M1_FAST (split-K fast kernel), M1_ROWS (long K) or M1_GENERAL
+    M1_WORK_QUEUE (wide matrices: chunks of 4 k-tiles taken from an LDS counter, per-chunk partial
+    sums added per row in k order), M1_FAST (split-K fast kernel), M1_ROWS (long K) or M1_GENERAL
     (the general GEMV kernel; no fused RMSNorm there)."""
     r = load_library().qlin_gemv_m1_route(N, K, bits, group)
     if r < 0:

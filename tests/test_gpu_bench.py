@@ -35,7 +35,7 @@ def test_bench_gpus2_spawns_ranks(split):
     """--gpus 2 (weak: an independent ring per rank; --split: output rows of one shared ring):
     two ranks ran, n_gpus is 2 and value is the whole-job throughput."""
     args = ["--gpus", "2", "--steps", "6", "--warmup", "2", "--ring", "16", "--ramp-s", "0.05",
-            "--no-cpu-baseline", "--no-decode-layer", "--no-other-mode"]
+            "--no-cpu-baseline", "--no-decode-layer", "--no-other-mode", "--pipeline", "off"]
     if split:
         args.append("--split")
     d = _bench(*args, extra_env={"BENCH_DIST_BACKEND": "gloo", "BENCH_SHARE_GPU": "1"})
@@ -50,3 +50,22 @@ def test_bench_gpus2_spawns_ranks(split):
         assert d["config"]["N_per_rank"] == 2048
     got = flops / (d["ms_per_step"] * 6 / 1e3) / 1e12
     assert abs(got - d["value"]) <= 0.02 * d["value"] + 1e-3, (got, d["value"])
+
+
+@pytest.mark.timeout(1100)
+def test_bench_gpus2_pipeline_leg():
+    """The configs[4] leg the driver's multi-GPU runs add to the line: with
+    two ranks the 32 LLaMA3-8B layers run as 2 pipeline stages (here gloo + one shared MI355X;
+    RCCL over xGMI, one rank per GPU, in the driver's runs), windows in flight and graph-replayed
+    decode steps are timed, and the pipeline's NLL and greedy tokens equal one process bit for
+    bit."""
+    d = _bench("--gpus", "2", "--steps", "2", "--warmup", "1", "--ring", "8", "--ramp-s", "0.05",
+               "--no-cpu-baseline", "--no-decode-layer", "--no-other-mode", "--pipe-windows", "2",
+               "--pipe-decode", "8", extra_env={"BENCH_DIST_BACKEND": "gloo",
+                                                 "BENCH_SHARE_GPU": "1"}, timeout=1000)
+    assert d["n_gpus"] == 2
+    p = d["pipeline"]
+    assert p["stages"] == [[0, 16], [16, 32]] and p["backend"] == "gloo"
+    assert p["windows"]["ms_per_window"] > 0 and p["decode"]["ms_per_step"] > 0
+    assert p["check"]["nll_bit_identical_to_one_process"], p["check"]
+    assert p["check"]["tokens_identical_to_one_process"], p["check"]

@@ -466,3 +466,32 @@ def test_gemv_batched_rejects_overlapping_strides():
     assert ok == 1  # zero weight strides would alias problems
     with pytest.raises(ValueError):
         qlin.gemv_batched(x, qw.unsqueeze(0), qsz.unsqueeze(0), None, 64, 256, 4, 128, fl)
+
+
+def test_gemv_batched_geometry_per_instance():
+    """Each streaming-kernel instance sizes its grid from its OWN static LDS and occupancy
+    (a cache keyed on the kernel's C++ type was shared by every instance, so the first
+    launch in a process decided the LDS padding and blocks per CU of all later ones).  Plan int4
+    g128 first, then the two-row int2 g32 / g64 and int3 g64 instances (larger static LDS), then a
+    one-row instance (odd tile-row count): every two-row instance must hold exactly 4 blocks per
+    CU with its own padding, and no plan may promise more blocks per CU than its LDS allows."""
+    K, B = 4096, 8
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    x = torch.zeros(B, 1, K, dtype=torch.float16, device="cuda")
+    seen = {}
+    for N, bits, group in ((4096, 4, 128), (4096, 2, 32), (4096, 2, 64), (4096, 3, 64),
+                           (4112, 4, 128), (4096, 4, 128)):
+        qw = torch.zeros(B, *qlin.packed_shape(N, K, bits), dtype=torch.int32, device="cuda")
+        qsz = torch.zeros(B, *qlin.sz_shape(N, K, group), dtype=torch.int32, device="cuda")
+        p = qlin.gemv_batched_plan(x, qw, qsz, N, K, bits, group)
+        assert p["blocks"] > 0, (N, bits, group, p)
+        lds = p["static_lds"] + p["dyn_lds"]
+        assert p["blocks_per_cu"] * lds <= 160 * 1024, (N, bits, group, p)
+        if p["rows_per_wave"] == 2:
+            assert p["blocks_per_cu"] == 4 and lds == 40 * 1024 - 64, (N, bits, group, p)
+        else:
+            assert N == 4112 and p["dyn_lds"] == 0, (N, bits, group, p)
+        tiles = B * (-(-N // 16)) // p["rows_per_wave"]
+        assert p["blocks"] == -(-min(tiles, cus * p["blocks_per_cu"] * 4) // 4), p
+        key = (N, bits, group)
+        assert seen.setdefault(key, p) == p  # the same instance plans the same way every time

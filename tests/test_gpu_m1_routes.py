@@ -1,8 +1,9 @@
 """Every one-token-row route of the packed linear against the oracle.
 
 At M = 1 the library routes each shape to one of three kernels (``qlin_gemv_m1_route``,
-csrc/qlin_gemv.hip ``m1_route``): the whole-row kernel (wide matrices: LLaMA3-8B gate/up, N =
-28,672, and N = 16,384), the fast split-K kernel (q/k/v, o, 4096^2) and the rows kernel (long K:
+csrc/qlin_gemv.hip ``m1_route``): the work-queue kernel (wide matrices: LLaMA3-8B gate/up, N =
+28,672, and N = 16,384; chunks of 4 k-tiles from an LDS counter, per-chunk partial sums added per
+row in k order), the fast split-K kernel (q/k/v, o, 4096^2) and the rows kernel (long K:
 the down projection, 4096 x 14,336).  Here each route meets ``O.linear_ref`` (the reference's
 ``F.linear(x, W_dq)``, quant/int_linear.py:62, in float64) directly, at every bit width {2, 3, 4,
 8} x group {32, 64, 128} and every zero-point mode of the layout: integral zeros (the
@@ -28,8 +29,8 @@ pytestmark = pytest.mark.gpu
 
 from quant import qlin  # noqa: E402
 
-SHAPES = {"gate_up_28672x4096": (28672, 4096, qlin.M1_WHOLE_ROW),
-          "wide_16384x4096": (16384, 4096, qlin.M1_WHOLE_ROW),
+SHAPES = {"gate_up_28672x4096": (28672, 4096, qlin.M1_WORK_QUEUE),
+          "wide_16384x4096": (16384, 4096, qlin.M1_WORK_QUEUE),
           "down_4096x14336": (4096, 14336, qlin.M1_ROWS),
           "qkv_6144x4096": (6144, 4096, qlin.M1_FAST)}
 BITS_GROUPS = [(b, g) for b in (2, 3, 4, 8) for g in (32, 64, 128)]
@@ -134,7 +135,7 @@ def test_m1_route_integral_zeros(name, bits, group):
 
 
 @pytest.mark.parametrize("bits,group", [(4, 128), (3, 64), (2, 32), (8, 64)])
-def test_m1_route_whole_row_16384(bits, group):
+def test_m1_route_work_queue_16384(bits, group):
     _check_routes("wide_16384x4096", bits, group, "narrow")
 
 

@@ -72,7 +72,7 @@ def test_invalid_arguments_return_einval_without_a_gpu():
     assert lib.qlin_rmsnorm_linear_ep_f16(p, p, 0, p, p, 1e-5, None, None, p, 1, 16, 256, 4, 128,
                                           1, None) == 1  # residual epilogue without residual
     # ABI 12: which M = 1 kernel a shape takes (without a device: the 256-CU MI355X geometry)
-    assert lib.qlin_gemv_m1_route(28672, 4096, 4, 128) == 1   # gate/up: whole-row kernel
+    assert lib.qlin_gemv_m1_route(28672, 4096, 4, 128) == 1   # gate/up: work-queue kernel
     assert lib.qlin_gemv_m1_route(6144, 4096, 3, 64) == 2     # q/k/v: fast kernel
     assert lib.qlin_gemv_m1_route(4096, 14336, 2, 32) == 3    # down: rows kernel
     assert lib.qlin_gemv_m1_route(4096, 1000, 4, 40) == -1    # invalid layout

@@ -1,8 +1,17 @@
 #!/usr/bin/env python3
 """HBM bytes per decode layer from a rocprofv3 --pmc FETCH_SIZE pass over bench.py's decode-layer
-line (run with --no-other-mode: then every GEMV / attention dispatch of the run belongs to the
-decode layers).  bytes per layer = sum over those dispatches of FETCH_SIZE x 1024 x 2 (the gfx950
-correction, MI355X_MICROARCH.md HBM section) / number of attention dispatches (one per layer).
+line (run with --no-other-mode --ramp-s 0).
+
+Every dispatch of the layer pass counts, whatever its kernel is called (an
+allow-list of kernel names missed the round-5 gate/up kernel and published half the bytes).  The
+dispatches are taken in dispatch order; each attention dispatch (``attn_decode``: one per layer)
+marks a layer, whose window runs from the dispatch just before it (the q/k/v launch) to the
+dispatch before the next layer's q/k/v launch; the last layer's window is as long as the others.
+The tool fails unless every window has the same shape of at least five dispatches — q/k/v, the
+attention, o, gate/up, down — with the attention second and GEMV kernels in the other four places.
+
+bytes per layer = mean over the windows of sum(FETCH_SIZE x 1024 x 2) (the gfx950 correction,
+MI355X_MICROARCH.md HBM section).
 Usage: python tools/decode_traffic.py <pmc dir> <out.json>"""
 import collections
 import csv
@@ -11,29 +20,72 @@ import json
 import os
 import sys
 
-LAYER_KERNELS = ("gemv_fast_kernel", "gemv_kernel", "gemv_wrow_kernel", "gemv_rows_kernel",
-                 "attn_decode_kernel")
+CLASSES = ("qkv_norm", "attention", "o_residual", "gate_up_norm_silu", "down_residual")
+
+
+def _rows(d):
+    rows = []
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
+        for i, r in enumerate(csv.DictReader(open(f))):
+            if r.get("Counter_Name") != "FETCH_SIZE":
+                continue
+            key = (int(r["Dispatch_Id"]) if r.get("Dispatch_Id", "").isdigit()
+                   else int(r.get("Start_Timestamp") or i))
+            rows.append((key, r.get("Kernel_Name", ""), float(r["Counter_Value"]) * 1024 * 2))
+    rows.sort(key=lambda t: t[0])
+    return rows
+
+
+def layer_windows(rows):
+    """[(names, bytes)] per layer window (see the module docstring); raises SystemExit when the
+    pass does not have the decode layer's shape."""
+    att = [i for i, r in enumerate(rows) if "attn_decode" in r[1]]
+    if len(att) < 2:
+        raise SystemExit("fewer than two attention dispatches: not a decode-layer pass")
+    if att[0] < 1:
+        raise SystemExit("no q/k/v dispatch before the first attention dispatch")
+    spans = [att[j + 1] - att[j] for j in range(len(att) - 1)]
+    width = collections.Counter(spans).most_common(1)[0][0]
+    wins = []
+    for j, a in enumerate(att):
+        end = att[j + 1] - 1 if j + 1 < len(att) else a - 1 + width
+        if end > len(rows):
+            raise SystemExit(f"last layer window runs past the pass ({end} > {len(rows)})")
+        wins.append(rows[a - 1:end])
+    shapes = collections.Counter(len(w) for w in wins)
+    if len(shapes) != 1:
+        raise SystemExit(f"layer windows of different lengths {dict(shapes)}: another kernel ran "
+                         "inside the decode pass (run bench.py with --no-other-mode)")
+    n = wins[0].__len__()
+    if n < len(CLASSES):
+        raise SystemExit(f"{n} dispatches per layer: fewer than the five kernel classes {CLASSES}")
+    for w in wins:
+        names = [r[1] for r in w]
+        if "attn_decode" not in names[1] or any("gemv" not in names[p] for p in (0, 2, 3, 4)):
+            raise SystemExit(f"unexpected layer window {names}")
+    return wins
 
 
 def main():
     d, out = sys.argv[1:3]
-    per = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") != "FETCH_SIZE":
-                continue
-            name = r.get("Kernel_Name", "")
-            if any(k in name for k in LAYER_KERNELS):
-                per[name].append(float(r["Counter_Value"]) * 1024 * 2)
-    layers = sum(len(v) for k, v in per.items() if "attn_decode_kernel" in k)
-    if not layers:
-        raise SystemExit("no attention dispatches: not a decode-layer pass")
-    total = sum(sum(v) for v in per.values())
-    res = {"workload": "decode_layer_int4_g128", "layers_dispatched": layers,
-           "fetch_bytes_per_launch": total / layers,
-           "per_kernel_mean_bytes": {k[:120]: sum(v) / len(v) for k, v in per.items()},
-           "per_kernel_dispatches": {k[:120]: len(v) for k, v in per.items()},
+    rows = _rows(d)
+    if not rows:
+        raise SystemExit(f"no FETCH_SIZE rows under {d}")
+    wins = layer_windows(rows)
+    n = len(wins[0])
+    per_pos = [[w[p][2] for w in wins] for p in range(n)]
+    cls = list(CLASSES) + [f"extra_{p}" for p in range(len(CLASSES), n)]
+    total = sum(sum(r[2] for r in w) for w in wins) / len(wins)
+    res = {"workload": "decode_layer_int4_g128", "layers_dispatched": len(wins),
+           "dispatches_per_layer": n,
+           "fetch_bytes_per_launch": total,
+           "fetch_bytes_per_layer": total,
+           "per_class_mean_bytes": {c: sum(v) / len(v) for c, v in zip(cls, per_pos)},
+           "per_class_kernel": {c: wins[-1][p][1][:160] for p, c in enumerate(cls)},
+           "kernel_classes": n,
            "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 counts half of wide streaming reads)",
+           "method": ("every dispatch of each layer window (the q/k/v dispatch before an attention "
+                      "dispatch up to the next layer's q/k/v), dispatch order; mean over windows"),
            "source": "rocprofv3 --pmc FETCH_SIZE, separate pass, bench.py --no-other-mode"}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
