@@ -318,9 +318,10 @@ class PipelineRunner:
         """Σ NLL of each window (main.py:136-146) computed on the last stage and broadcast to all
         ranks, so every rank can form the perplexity."""
         n = len(windows) if windows is not None else None
-        n_t = torch.tensor([n if n is not None else 0], dtype=torch.int64, device=self.device)
-        self._bcast(n_t, 0)
-        n = int(n_t.item())
+        if self.info.world > 1:
+            n_t = torch.tensor([n if n is not None else 0], dtype=torch.int64, device=self.device)
+            self._bcast(n_t, 0)
+            n = int(n_t.item())
         logits = self.forward(windows if self.info.first else None, n_micro=n)
         from .quant_llama import nll_from_logits
         nll = torch.zeros(n, dtype=torch.float32, device=self.device)
@@ -331,7 +332,8 @@ class PipelineRunner:
                 nll[i] = nll_from_logits(lg, labels[i])
         elif self.info.first:
             self._send_labels(windows)
-        self._bcast(nll, self.info.world - 1)
+        if self.info.world > 1:
+            self._bcast(nll, self.info.world - 1)
         return nll
 
     def _send_labels(self, windows):

@@ -64,9 +64,21 @@ def test_decode_traffic_refuses_a_four_kernel_layer(tmp_path):
 def test_decode_traffic_refuses_ragged_windows(tmp_path):
     _write_pass(str(tmp_path / "pmc"), 6)
     rows = decode_traffic._rows(str(tmp_path / "pmc"))
-    rows.insert(12, (10**6, "void at::native::elementwise_kernel<...>", 1.0))
+    for at in (27, 17, 7):  # another kernel inside three of the six layers: no dominant shape
+        rows.insert(at, (10**6 + at, "void at::native::elementwise_kernel<...>", 1.0))
     with pytest.raises(SystemExit):
         decode_traffic.layer_windows(rows)
+
+
+def test_decode_traffic_leaves_out_the_eager_pass(tmp_path):
+    """One eager warm-up layer with two extra host-side torch kernels among 12 replayed ones: that
+    window is left out, never mixed into the bytes per layer."""
+    _write_pass(str(tmp_path / "pmc"), 12)
+    rows = decode_traffic._rows(str(tmp_path / "pmc"))
+    rows[8:8] = [(-1, "void at::native::elementwise_kernel<...>", 5e6)] * 2  # after layer 0
+    wins = decode_traffic.layer_windows(rows)
+    assert len(wins) == 11 and all(len(w) == 5 for w in wins)
+    assert sum(r[2] for r in wins[0]) == pytest.approx(sum(b for _, b in LAYER))
 
 
 def test_bench_never_publishes_traffic_below_algorithmic_bytes():

