@@ -7,6 +7,8 @@ allow-list of kernel names missed the round-5 gate/up kernel and published half 
 dispatches are taken in dispatch order; each attention dispatch (``attn_decode``: one per layer)
 marks a layer, whose window runs from the dispatch just before it (the q/k/v launch) to the
 dispatch before the next layer's q/k/v launch; the last layer's window is as long as the others.
+Round 6: with the q/k/v projection and the attention fused into one launch (``qkv_attn``) that
+launch marks the layer and starts its window, and a layer has four kernel classes.
 The windows of the timed graph-replayed passes must share one shape (>= 80 % of all windows: the
 eager warm-up pass, which also runs the layer's host-side torch ops, is reported and left out) of
 at least five dispatches — q/k/v, the attention, o, gate/up, down — with the attention second and
@@ -23,6 +25,17 @@ import os
 import sys
 
 CLASSES = ("qkv_norm", "attention", "o_residual", "gate_up_norm_silu", "down_residual")
+# round 6: the input RMSNorm + q/k/v + attention as ONE launch (qkv_attn_kernel)
+CLASSES_FUSED = ("qkv_norm_attention", "o_residual", "gate_up_norm_silu", "down_residual")
+
+
+def _marker(name):
+    return "attn_decode" in name or "qkv_attn" in name
+
+
+def _classes(rows):
+    fused = any("qkv_attn" in r[1] for r in rows)
+    return (CLASSES_FUSED, 0) if fused else (CLASSES, 1)  # (classes, marker's place in a layer)
 
 
 def _rows(d):
@@ -39,26 +52,27 @@ def _rows(d):
 
 
 def layer_windows_all(rows):
-    att = [i for i, r in enumerate(rows) if "attn_decode" in r[1]]
+    att = [i for i, r in enumerate(rows) if _marker(r[1])]
     return collections.Counter((att[j + 1] - att[j]) for j in range(len(att) - 1))
 
 
 def layer_windows(rows):
     """[(names, bytes)] per layer window (see the module docstring); raises SystemExit when the
     pass does not have the decode layer's shape."""
-    att = [i for i, r in enumerate(rows) if "attn_decode" in r[1]]
+    classes, at = _classes(rows)
+    att = [i for i, r in enumerate(rows) if _marker(r[1])]
     if len(att) < 2:
         raise SystemExit("fewer than two attention dispatches: not a decode-layer pass")
-    if att[0] < 1:
+    if att[0] < at:
         raise SystemExit("no q/k/v dispatch before the first attention dispatch")
     spans = [att[j + 1] - att[j] for j in range(len(att) - 1)]
     width = collections.Counter(spans).most_common(1)[0][0]
     wins = []
     for j, a in enumerate(att):
-        end = att[j + 1] - 1 if j + 1 < len(att) else a - 1 + width
+        end = att[j + 1] - at if j + 1 < len(att) else a - at + width
         if end > len(rows):
             raise SystemExit(f"last layer window runs past the pass ({end} > {len(rows)})")
-        wins.append(rows[a - 1:end])
+        wins.append(rows[a - at:end])
     shapes = collections.Counter(len(w) for w in wins)
     n, count = shapes.most_common(1)[0]
     # the graph-replayed passes (bench.py's timed decode line) are the bulk of the windows; the
@@ -69,11 +83,13 @@ def layer_windows(rows):
         raise SystemExit(f"layer windows of different lengths {dict(shapes)}: no dominant decode "
                          "pass (run bench.py with --no-other-mode)")
     wins = [w for w in wins if len(w) == n]
-    if n < len(CLASSES):
-        raise SystemExit(f"{n} dispatches per layer: fewer than the five kernel classes {CLASSES}")
+    if n < len(classes):
+        raise SystemExit(f"{n} dispatches per layer: fewer than the {len(classes)} kernel classes "
+                         f"{classes} (five kernel classes unless q/k/v + attention are fused)")
     for w in wins:
         names = [r[1] for r in w]
-        if "attn_decode" not in names[1] or any("gemv" not in names[p] for p in (0, 2, 3, 4)):
+        if not _marker(names[at]) or any("gemv" not in names[p] for p in range(len(classes))
+                                         if p != at):
             raise SystemExit(f"unexpected layer window {names}")
     return wins
 
@@ -86,8 +102,9 @@ def main():
     all_wins = layer_windows_all(rows)
     wins = layer_windows(rows)
     n = len(wins[0])
+    classes, _ = _classes(rows)
     per_pos = [[w[p][2] for w in wins] for p in range(n)]
-    cls = list(CLASSES) + [f"extra_{p}" for p in range(len(CLASSES), n)]
+    cls = list(classes) + [f"extra_{p}" for p in range(len(classes), n)]
     total = sum(sum(r[2] for r in w) for w in wins) / len(wins)
     res = {"workload": "decode_layer_int4_g128", "layers_dispatched": len(wins),
            "dispatches_per_layer": n,
@@ -96,6 +113,7 @@ def main():
            "per_class_mean_bytes": {c: sum(v) / len(v) for c, v in zip(cls, per_pos)},
            "per_class_kernel": {c: wins[-1][p][1][:160] for p, c in enumerate(cls)},
            "kernel_classes": n,
+           "layout": "fused q/k/v + attention" if len(classes) == 4 else "five launches",
            "window_lengths_seen": {str(k): v for k, v in sorted(all_wins.items())},
            "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 counts half of wide streaming reads)",
            "method": ("every dispatch of each layer window (the q/k/v dispatch before an attention "
