@@ -323,29 +323,15 @@ def decode_layer_bench(args, dev, timed):
         del graph
         return el / (steps * reps * R) * 1e6
 
-    # the product path: q/k/v + attention as one launch (4 launches per layer) where the shapes
-    # allow; the two-launch form of the same layer beside it (round-5 product, 5 launches)
-    fused = all(layer.self_attn._qkv_attn_norm(x, layer.input_layernorm, kv + 1) is not None
-                for layer in layers)
     us = time_graph()
-    for layer in layers:
-        layer.self_attn.fused_qkv_attn = False
-    us_two = time_graph()
-    for layer in layers:
-        layer.self_attn.fused_qkv_attn = True
     nbytes, flops = decode_layer_bytes(cfg, kv + 1)
     out = {"workload": "decode_layer_int4_g128",
            "what": ("LLaMA3-8B decoder layer, batch-1 decode step, int4 g128 packed + fused "
-                    "(RMSNorm+q/k/v+RoPE+KV append+attention in one launch, o+residual, "
-                    "gate/up+RMSNorm+SiLU*up, down+residual: 4 launches), graph-replayed over "
-                    "distinct layers" if fused else
-                    "LLaMA3-8B decoder layer, batch-1 decode step, int4 g128 packed + fused "
                     "(q/k/v+RMSNorm, attention+RoPE+KV append, o+residual, gate/up+RMSNorm+SiLU*up, "
                     "down+residual: 5 launches), graph-replayed over distinct layers"),
            "layers": R, "layers_per_graph": reps * R, "kv_len": kv + 1,
-           "launches_per_layer": 4 if fused else 5,
+           "launches_per_layer": 5,
            "us_per_layer": round(us, 2),
-           "two_launch_qkv_attention_us_per_layer": round(us_two, 2),
            "est_32_layer_token_ms": round(us * 32 / 1e3, 3),
            "tflops": round(flops / us / 1e6, 3),
            "roofline": {"bound": "hbm", "achieved": round(nbytes / us / 1e3, 1),

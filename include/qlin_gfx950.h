@@ -326,38 +326,6 @@ int qlin_attn_decode_rope_len(const uint16_t* q, int64_t q_row_stride, const uin
                               const int32_t* len, void* stream);
 
 /*
- * The decoder layer's input RMSNorm + fused q/k/v projection AND its decode attention (RoPE, the
- * KV-cache append, split-L attention) for ONE token row, in one launch (ABI 13): the arithmetic of
- * qlin_rmsnorm_linear_ep_f16 (QLIN_EP_NONE) followed by qlin_attn_decode_rope /
- * qlin_attn_decode_rope_len — models/int_llama_layer.py:113-165 of the reference at q_len 1.
- * Each KV head's attention blocks wait only for that head's q / k / v row tiles (a head-local
- * hand-off inside the launch) while their cached K / V rows stream in.
- *   qweight / qsz / flags: the fused q/k/v weight (rows q | k | v, N = (Hq + 2 Hkv) D), flags
- *   must include QLIN_NORM_W16 (norm_weight: the fp16 RMSNorm weight [K], eps its epsilon);
- *   x fp16 [K] (the hidden state before the norm); qkv_out fp16 [N]: the projection rows, written
- *   (before RoPE).  cos / sin / position_ids / caches / mask / out / scale_div as
- *   qlin_attn_decode_rope with B = 1; len NULL: the cache holds L - 1 rows and receives row L - 1;
- *   len non-NULL: as qlin_attn_decode_rope_len (L = the capacity L_cap, mask NULL, position_ids
- *   required).  partials: qlin_qkv_attn_partials_bytes(Hq, Hkv, L) bytes (NULL when 0);
- *   counters int32 [>= 2 Hkv], zero-filled before the first use and left zero by every call (one
- *   buffer per stream, graph replays included).
- *   qlin_qkv_attn_supported(): 1 when the launch takes these shapes (today: Hq = 4 Hkv, D = 128,
- *   K a multiple of 128 with 3-4 k-tiles per wave of an 8-wave block — LLaMA3-8B's 4096 — the
- *   flags with QLIN_NORM_W16, L <= 4096), else 0: the caller runs the two launches.
- */
-int qlin_qkv_attn_supported(int Hq, int Hkv, int D, int64_t K, int bits, int group, int flags,
-                            int64_t L);
-int64_t qlin_qkv_attn_partials_bytes(int Hq, int Hkv, int64_t L);
-int qlin_qkv_attn_decode_f16(const uint32_t* qweight, const uint32_t* qsz, int flags,
-                             const uint16_t* x, const uint16_t* norm_weight, float eps,
-                             uint16_t* qkv_out, const float* cos_cache, const float* sin_cache,
-                             int64_t cache_rows, const int64_t* position_ids, uint16_t* k_cache,
-                             uint16_t* v_cache, int64_t kv_head_stride, const uint16_t* mask,
-                             void* out, int out_dtype, int Hq, int Hkv, int64_t L, int D,
-                             int64_t K, int bits, int group, float scale_div, float* partials,
-                             int32_t* counters, const int32_t* len, void* stream);
-
-/*
  * Fused prefill attention (many query tokens per sequence): the same attention core as
  * qlin_attn_decode — repeat_kv, fp32 QK^T, / sqrt(head_dim) (as torch: x the fp32 reciprocal),
  * + mask, clamp at finfo(fp32).min, fp32 softmax, fp32 PV (models/int_llama_layer.py:137-165 of

@@ -305,36 +305,6 @@ class QuantLlamaAttention(nn.Module):
     _dyn_len = None
     _dyn_max = None
 
-    # the input RMSNorm + q/k/v projection + RoPE + KV append + decode attention of one token as
-    # ONE launch (qlin.qkv_attn_decode) where the shapes allow; False: the two launches
-    fused_qkv_attn = True
-
-    def _qkv_attn_norm(self, hidden_states, prenorm, L):
-        """(fp16 norm weight, eps) when this one-token step takes qlin.qkv_attn_decode, else None."""
-        if not (self.fused_qkv_attn and self.qkv is not None and prenorm is not None
-                and self.qkv.bias is None and self.head_dim == qlin.ATTN_D
-                and hidden_states.shape[0] == 1):
-            return None
-        if _same_act([self.q_proj, self.k_proj, self.v_proj]) != (0, 0):
-            return None
-        norm = prenorm.fusable(hidden_states)
-        if norm is None or norm[0].dtype != torch.float16 or not self.qkv.prenorm_ok(hidden_states):
-            return None
-        if not qlin.qkv_attn_supported(self.num_heads, self.num_key_value_heads, self.head_dim,
-                                       self.qkv.in_features, self.qkv.wbits, self.qkv.group,
-                                       self.qkv.qflags, L):
-            return None
-        return norm
-
-    def _qkv_attn(self, hidden_states, norm, cos_c, sin_c, position_ids, buf, **kw):
-        q = self.qkv
-        attn, _ = qlin.qkv_attn_decode(hidden_states.contiguous(), norm[0], norm[1], q.qweight,
-                                       q.qsz, q.qflags, q.wbits, q.group, cos_c, sin_c,
-                                       position_ids, self.num_heads, self.num_key_value_heads,
-                                       self.head_dim, buf[0], buf[1], out_dtype=torch.float16,
-                                       scale_div=math.sqrt(self.head_dim), **kw)
-        return attn.transpose(1, 2).reshape(1, 1, self.hidden_size)
-
     def _decode_step_len(self, hidden_states, position_ids, residual, prenorm):
         """One token through the fused packed attention with the cache length on the device
         (qlin_attn_decode_rope_len over self._kv's capacity): a launch sequence that stays valid
@@ -344,14 +314,8 @@ class QuantLlamaAttention(nn.Module):
         if not (self.kv_cache and self._kv is not None and act_dtype == torch.float16
                 and position_ids is not None):
             raise ValueError("device-length decode needs kv_cache buffers, fp16 and position_ids")
-        buf = self._kv
-        norm = self._qkv_attn_norm(hidden_states, prenorm, self._dyn_max or buf[0].shape[2])
-        if norm is not None:
-            cos_c, sin_c = self._rope_cache(buf[0], buf[0].shape[2])
-            attn = self._qkv_attn(hidden_states, norm, cos_c, sin_c, position_ids, buf,
-                                  length=self._dyn_len, max_len=self._dyn_max)
-            return self._out(attn, residual), None, None
         q, k, v = self._project(hidden_states, prenorm)
+        buf = self._kv
         cos_c, sin_c = self._rope_cache(buf[0], buf[0].shape[2])
         attn = qlin.attn_decode_rope_len(q, k, v, cos_c, sin_c, position_ids, self.num_heads,
                                          self.num_key_value_heads, self.head_dim, buf[0], buf[1],
@@ -396,15 +360,6 @@ class QuantLlamaAttention(nn.Module):
             position_ids = torch.arange(kv_seq_len - q_len, kv_seq_len, device=hidden_states.device)[None]
         decode = self._decode_kernel_ok(hidden_states, attention_mask, past_key_value, use_cache,
                                         output_attentions, kv_seq_len)
-        norm = self._qkv_attn_norm(hidden_states, prenorm, kv_seq_len) if decode else None
-        if norm is not None:
-            # one launch: input RMSNorm, q/k/v, RoPE, the cache append and the decode attention
-            buf, L0 = self._cache_for(past_key_value, bsz, 1, hidden_states.device)
-            cos_c, sin_c = self._rope_cache(hidden_states, kv_seq_len)
-            attn_output = self._qkv_attn(hidden_states, norm, cos_c, sin_c, position_ids, buf,
-                                         kv0=L0, mask=attention_mask)
-            past_key_value = (buf[0][:, :, :L0 + 1], buf[1][:, :, :L0 + 1]) if use_cache else None
-            return self._out(attn_output, residual), None, past_key_value
         q, k, v = self._project(hidden_states, prenorm)
         value_states = v.reshape(bsz, q_len, self.num_key_value_heads, self.head_dim).transpose(1, 2)
         appended = False

@@ -74,11 +74,6 @@ SIGNATURES = {
                           _p],
                          _i),
     "qlin_attn_decode_splits": ([_l, _i, _l], _i),
-    "qlin_qkv_attn_supported": ([_i, _i, _i, _l, _i, _i, _i, _l], _i),
-    "qlin_qkv_attn_partials_bytes": ([_i, _i, _l], _l),
-    "qlin_qkv_attn_decode_f16": ([_p, _p, _i, _p, _p, ctypes.c_float, _p, _p, _p, _l, _p, _p, _p,
-                                  _l, _p, _p, _i, _i, _i, _l, _i, _l, _i, _i, ctypes.c_float, _p,
-                                  _p, _p, _p], _i),
     "qlin_attn_decode_rope_len": ([_p, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p, _p, _l, _p, _i,
                                    _l, _i, _i, _l, _i, ctypes.c_float, _p, _p, _p, _p], _i),
 }
@@ -810,74 +805,6 @@ def attn_decode_rope_len(q, k, v, cos_cache, sin_cache, position_ids, n_heads, n
         _ptr(length), _stream(q))
     _check(rc, "qlin_attn_decode_rope_len")
     return out
-
-
-def qkv_attn_supported(n_heads, n_kv_heads, head_dim, K, bits, group, flags, L):
-    """Whether ``qkv_attn_decode`` takes these shapes (``qlin_qkv_attn_supported``)."""
-    return bool(load_library().qlin_qkv_attn_supported(n_heads, n_kv_heads, head_dim, K, bits,
-                                                       group, flags | NORM_W16, L))
-
-
-def qkv_attn_decode(x, norm_weight, eps, qweight, qsz, flags, bits, group, cos_cache, sin_cache,
-                    position_ids, n_heads, n_kv_heads, head_dim, k_cache, v_cache, kv0=None,
-                    mask=None, length=None, max_len=None, out_dtype=torch.float16,
-                    scale_div=None):
-    """``qlin_qkv_attn_decode_f16``: the input RMSNorm + fused q/k/v projection + RoPE + KV append
-    + decode attention of ONE token in one launch.  x fp16 [1, 1, K] (before the norm),
-    norm_weight fp16 [K]; qweight / qsz the fused q/k/v weight (rows q | k | v).  Host length:
-    ``kv0`` = rows already cached (row kv0 is written), ``mask`` fp16 [1, 1, 1, kv0 + 1] or None.
-    Device length (graph replays): ``length`` int32 [1] with ``max_len`` (default: the cache
-    capacity), as ``attn_decode_rope_len``.  Returns (out [1, Hq, 1, D], qkv fp16 [1, 1, N])."""
-    _on_gpu(x, norm_weight, qweight, qsz, cos_cache, sin_cache, position_ids, k_cache, v_cache,
-            mask, length)
-    K = x.shape[-1]
-    N = (n_heads + 2 * n_kv_heads) * head_dim
-    if x.dtype != torch.float16 or x.numel() != K or norm_weight.dtype != torch.float16 or \
-            norm_weight.numel() != K:
-        raise ValueError("qkv_attn_decode: one fp16 token row and its fp16 norm weight")
-    _check_packed(qweight, qsz, N, K, bits, group)
-    if not (k_cache.is_contiguous() and v_cache.is_contiguous()) or k_cache.shape != v_cache.shape \
-            or tuple(k_cache.shape[:2]) != (1, n_kv_heads) or k_cache.shape[3] != head_dim or \
-            k_cache.dtype != torch.float16:
-        raise ValueError("qkv_attn_decode takes contiguous fp16 [1, Hkv, rows, D] caches")
-    if cos_cache.dtype != torch.float32 or not cos_cache.is_contiguous() or \
-            sin_cache.dtype != torch.float32 or not sin_cache.is_contiguous():
-        raise ValueError("qkv_attn_decode takes contiguous fp32 cos / sin caches")
-    rows = k_cache.shape[2]
-    if length is not None:
-        if length.dtype != torch.int32 or position_ids is None or mask is not None:
-            raise ValueError("qkv_attn_decode: device length needs int32 length, position_ids, "
-                             "no mask")
-        L = rows if max_len is None else int(max_len)
-        if L < 1 or L > rows:
-            raise ValueError(f"qkv_attn_decode: max length {L} must fit the cache ({rows} rows)")
-    else:
-        L = kv0 + 1
-        if kv0 < 0 or L > rows:
-            raise ValueError(f"cache rows {rows} cannot take row {kv0}")
-    if not qkv_attn_supported(n_heads, n_kv_heads, head_dim, K, bits, group, flags, L):
-        raise ValueError("qkv_attn_decode: unsupported shapes")
-    pos, pbs = (None, 0) if position_ids is None else _pos_ids(position_ids, 1, 1)
-    m = None
-    if mask is not None:
-        if mask.dtype != torch.float16 or mask.shape[-1] != L or mask.numel() != L:
-            raise ValueError("qkv_attn_decode: mask fp16 [1, 1, 1, L]")
-        m = mask.reshape(1, L).contiguous()
-    lib = load_library()
-    out = torch.empty(1, n_heads, 1, head_dim, dtype=out_dtype, device=x.device)
-    qkv = torch.empty(1, 1, N, dtype=torch.float16, device=x.device)
-    nb = lib.qlin_qkv_attn_partials_bytes(n_heads, n_kv_heads, L)
-    part = torch.empty(nb // 4, dtype=torch.float32, device=x.device) if nb > 0 else None
-    cnt = _attn_counters(x.device, 2 * n_kv_heads)
-    sd = math.sqrt(head_dim) if scale_div is None else float(scale_div)
-    rc = lib.qlin_qkv_attn_decode_f16(
-        _ptr(qweight), _ptr(qsz), flags | NORM_W16, _ptr(x), _ptr(norm_weight), float(eps),
-        _ptr(qkv), _ptr(cos_cache), _ptr(sin_cache), cos_cache.shape[0], _ptr(pos),
-        _ptr(k_cache), _ptr(v_cache), rows * head_dim, _ptr(m), _ptr(out), _dtcode(out), n_heads,
-        n_kv_heads, L, head_dim, K, bits, group, ctypes.c_float(sd), _ptr(part), _ptr(cnt),
-        _ptr(length), _stream(x))
-    _check(rc, "qlin_qkv_attn_decode_f16")
-    return out, qkv
 
 
 def scale_div_default(head_dim):

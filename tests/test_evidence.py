@@ -81,17 +81,6 @@ def test_decode_traffic_leaves_out_the_eager_pass(tmp_path):
     assert sum(r[2] for r in wins[0]) == pytest.approx(sum(b for _, b in LAYER))
 
 
-def test_decode_traffic_fused_layer(tmp_path):
-    """The round-6 layer: q/k/v + attention as one launch that marks the layer: four classes."""
-    fused = [("void (anonymous namespace)::qkv_attn_kernel<4, 1, 0, 4>(FastArgs, AttnArgs)",
-              16.1e6)] + LAYER[2:]
-    _write_pass(str(tmp_path / "pmc"), 10, layer=fused)
-    rows = decode_traffic._rows(str(tmp_path / "pmc"))
-    wins = decode_traffic.layer_windows(rows)
-    assert len(wins) == 10 and all(len(w) == 4 for w in wins)
-    assert sum(r[2] for r in wins[3]) == pytest.approx(sum(b for _, b in fused))
-
-
 def test_bench_never_publishes_traffic_below_algorithmic_bytes():
     sys.path.insert(0, ROOT)
     import bench
@@ -117,8 +106,7 @@ def test_committed_decode_layer_pmc_has_every_kernel():
     import bench
     from transformers import LlamaConfig
     d = json.load(open(_newest("r*_decode_layer_int4_g128_pmc.json")))
-    fused = d.get("layout") == "fused q/k/v + attention"
-    assert d.get("kernel_classes", 0) >= (4 if fused else 5), d
+    assert d.get("kernel_classes", 0) >= 5, d
     cfg = LlamaConfig(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
                       num_key_value_heads=8)
     algo, _ = bench.decode_layer_bytes(cfg, 513)

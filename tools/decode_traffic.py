@@ -7,8 +7,6 @@ allow-list of kernel names missed the round-5 gate/up kernel and published half 
 dispatches are taken in dispatch order; each attention dispatch (``attn_decode``: one per layer)
 marks a layer, whose window runs from the dispatch just before it (the q/k/v launch) to the
 dispatch before the next layer's q/k/v launch; the last layer's window is as long as the others.
-Round 6: with the q/k/v projection and the attention fused into one launch (``qkv_attn``) that
-launch marks the layer and starts its window, and a layer has four kernel classes.
 The windows of the timed graph-replayed passes must share one shape (>= 80 % of all windows: the
 eager warm-up pass, which also runs the layer's host-side torch ops, is reported and left out) of
 at least five dispatches — q/k/v, the attention, o, gate/up, down — with the attention second and
@@ -25,17 +23,13 @@ import os
 import sys
 
 CLASSES = ("qkv_norm", "attention", "o_residual", "gate_up_norm_silu", "down_residual")
-# round 6: the input RMSNorm + q/k/v + attention as ONE launch (qkv_attn_kernel)
-CLASSES_FUSED = ("qkv_norm_attention", "o_residual", "gate_up_norm_silu", "down_residual")
-
 
 def _marker(name):
-    return "attn_decode" in name or "qkv_attn" in name
+    return "attn_decode" in name
 
 
 def _classes(rows):
-    fused = any("qkv_attn" in r[1] for r in rows)
-    return (CLASSES_FUSED, 0) if fused else (CLASSES, 1)  # (classes, marker's place in a layer)
+    return CLASSES, 1  # (classes, the attention's place in a layer)
 
 
 def _rows(d):
@@ -85,7 +79,7 @@ def layer_windows(rows):
     wins = [w for w in wins if len(w) == n]
     if n < len(classes):
         raise SystemExit(f"{n} dispatches per layer: fewer than the {len(classes)} kernel classes "
-                         f"{classes} (five kernel classes unless q/k/v + attention are fused)")
+                         f"{classes} (five kernel classes)")
     for w in wins:
         names = [r[1] for r in w]
         if not _marker(names[at]) or any("gemv" not in names[p] for p in range(len(classes))
@@ -113,7 +107,6 @@ def main():
            "per_class_mean_bytes": {c: sum(v) / len(v) for c, v in zip(cls, per_pos)},
            "per_class_kernel": {c: wins[-1][p][1][:160] for p, c in enumerate(cls)},
            "kernel_classes": n,
-           "layout": "fused q/k/v + attention" if len(classes) == 4 else "five launches",
            "window_lengths_seen": {str(k): v for k, v in sorted(all_wins.items())},
            "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 counts half of wide streaming reads)",
            "method": ("every dispatch of each layer window (the q/k/v dispatch before an attention "
