@@ -431,10 +431,13 @@ def pipeline_bench(args, dev, world, rank, backend):
            "what": (f"{nl} LLaMA3-8B decoder layers (4096 / 14336 / 32q 8kv / vocab 128,256), "
                     "RTN int4 g128 packed + fused, as contiguous pipeline stages, hidden states "
                     f"handed stage to stage by {'RCCL (xGMI) ' if backend == 'nccl' else ''}"
-                    f"{backend} send / recv"),
+                    f"{backend} send / recv" if multi else
+                    f"{nl} LLaMA3-8B decoder layers (4096 / 14336 / 32q 8kv / vocab 128,256), "
+                    "RTN int4 g128 packed + fused, one stage (the one-rank pipeline)"),
+           "backend": backend if multi else None,
            "stages": [[stage_info(nl, r, world).lo, stage_info(nl, r, world).hi]
                       for r in range(world)],
-           "backend": backend, "build_s_rank0": round(build_s, 2),
+           "build_s_rank0": round(build_s, 2),
            "windows": {"windows_in_flight": W, "tokens_per_window": T,
                        "ms_per_window": round(t_win / W * 1e3, 3),
                        "tokens_per_s": round(W * T / t_win, 1),

@@ -11,7 +11,7 @@ if len(sys.argv) > 2:
     rows = rows[-int(sys.argv[2]):]
 by = {}
 for name, s, e in rows:
-    short = name.split("(")[0].replace("(anonymous namespace)::", "")[:90]
+    short = name.replace("(anonymous namespace)::", "").split("(")[0][:90]
     by.setdefault(short, []).append((e - s) / 1e3)
 gaps = [(rows[i + 1][1] - rows[i][2]) / 1e3 for i in range(len(rows) - 1)]
 span = (rows[-1][2] - rows[0][1]) / 1e3
