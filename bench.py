@@ -81,14 +81,27 @@ def _pmc_traffic(workload):
     return d
 
 
-def _attach_traffic(roof, pmc, algo):
+def _attach_traffic(roof, pmc, algo, launch_products=None):
     """roofline.traffic from a committed PMC pass, or null: a pass that reports fewer HBM bytes
     than the launch's algorithmic bytes (every algorithmic byte is read at least once) missed
-    dispatches and is not published; traffic_ratio = traffic / algorithmic."""
+    dispatches and is not published; traffic_ratio = traffic / algorithmic.
+    A pass records the products one profiled launch computed (`products_per_launch`, the bench
+    ring); a line whose launches hold another number of products gets the pass's bytes per product
+    times its own (a strided batch streams each product's bytes once), and says so."""
     if pmc is None:
         return
     t = pmc["fetch_bytes_per_launch"]
     roof["traffic_source"] = pmc["file"]
+    if launch_products is not None:
+        p = pmc.get("products_per_launch")
+        if p is None:
+            roof["traffic"] = None
+            roof["traffic_rejected"] = f"{pmc['file']}: launch size of the pass not recorded"
+            return
+        if p != launch_products:
+            t = t / p * launch_products
+            roof["traffic_scaled"] = (f"per product from a pass at {p} products per launch, x "
+                                      f"{launch_products}")
     if t < algo:
         roof["traffic"] = None
         roof["traffic_rejected"] = (f"{pmc['file']}: {round(t)} B < {algo} algorithmic B per "
@@ -683,7 +696,7 @@ def main():
         r["traffic"] = None
         pmc_name = args.workload + ("_batched" if launch_products > 1 else "")
         pmc = _pmc_traffic(pmc_name) if not (args.split and world > 1) else None
-        _attach_traffic(r, pmc, nbytes * launch_products)
+        _attach_traffic(r, pmc, nbytes * launch_products, launch_products)
         r["bytes_per_launch"] = nbytes * launch_products
         r["bytes_read_per_launch"] = read_bytes * launch_products
         r["us_per_launch"] = round(per_product * launch_products * 1e6, 3)

@@ -111,3 +111,37 @@ def test_committed_decode_layer_pmc_has_every_kernel():
                       num_key_value_heads=8)
     algo, _ = bench.decode_layer_bytes(cfg, 513)
     assert 1.0 <= d["fetch_bytes_per_layer"] / algo <= 1.1, (d["fetch_bytes_per_layer"], algo)
+
+
+def test_bench_scales_traffic_to_the_lines_launch_size():
+    """A pass taken at one ring size published on a line at another (round 6: the two-rank
+    rehearsal's 8-product launches carried the 64-product pass, 8.1x algorithmic) is scaled per
+    product; a pass without its launch size is not published on a batched line."""
+    sys.path.insert(0, ROOT)
+    import bench
+    algo1 = bench.algo_bytes(1, 4096, 4096, 4, 128)
+    pmc = {"fetch_bytes_per_launch": 1.0145 * algo1 * 64, "products_per_launch": 64,
+           "file": "x.json"}
+    r = {}
+    bench._attach_traffic(r, dict(pmc), algo1 * 8, 8)
+    assert r["traffic_ratio"] == pytest.approx(1.0145, abs=1e-4) and "64" in r["traffic_scaled"]
+    r = {}
+    bench._attach_traffic(r, dict(pmc), algo1 * 64, 64)
+    assert "traffic_scaled" not in r and r["traffic_ratio"] == pytest.approx(1.0145, abs=1e-4)
+    r = {}
+    bench._attach_traffic(r, {"fetch_bytes_per_launch": 5e8, "file": "x.json"}, algo1 * 8, 8)
+    assert r["traffic"] is None and "not recorded" in r["traffic_rejected"]
+
+
+@pytest.mark.parametrize("workload", ["gemv_int4_g128", "gemv_int3_g64", "gemv_int2_g64",
+                                      "gemv_int3_g64_hqq", "gemv_int2_g64_hqq"])
+def test_committed_ring_pmc_per_product(workload):
+    """The newest committed batched-ring PMC pass of each GEMV workload reads every algorithmic
+    byte once, within 10 %, per product of the launch size it records."""
+    sys.path.insert(0, ROOT)
+    import bench
+    M, N, K, bits, group, ring, _, _ = bench.WORKLOADS[workload]
+    d = json.load(open(_newest(f"r*_{workload}_batched_pmc.json")))
+    assert d["products_per_launch"] == ring, d
+    ratio = d["fetch_bytes_per_launch"] / ring / bench.algo_bytes(M, N, K, bits, group)
+    assert 1.0 <= ratio <= 1.1, ratio

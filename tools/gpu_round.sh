@@ -37,12 +37,12 @@ for s in $STEPS; do
          -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode --ramp-s 0 > "$OUT/pmcd.log" 2>&1)
       rc=$?; echo "pmcd rc=$rc"; tail -2 "$OUT/pmcd.log"; ok_or_stop $rc pmcd
       python tools/decode_traffic.py "$OUT/pmcd" "$OUT/${R:-r6}_decode_layer_int4_g128_pmc.json"; rm -rf "$OUT/pmcd" ;;
-    pmchqq)  # FETCH_SIZE of the HQQ fp16-zero rings (configs[3])
+    pmchqq)  # FETCH_SIZE of the HQQ fp16-zero rings (configs[3]); ring per bench.py WORKLOADS
       for w in gemv_int3_g64_hqq gemv_int2_g64_hqq; do
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_$w" -o run \
            -- python "$ROOT/bench.py" --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode > "$OUT/pmc_$w.log" 2>&1)
         rc=$?; echo "pmc $w rc=$rc"; ok_or_stop $rc "pmc $w"
-        python tools/pmc_traffic.py "$OUT/pmc_$w" gemv_stream ${w}_batched "$OUT/${R:-r6}_${w}_batched_pmc.json"; rm -rf "$OUT/pmc_$w"
+        python tools/pmc_traffic.py "$OUT/pmc_$w" gemv_stream ${w}_batched "$OUT/${R:-r6}_${w}_batched_pmc.json" "$(case $w in *int2*) echo 96 ;; *) echo 64 ;; esac)"; rm -rf "$OUT/pmc_$w"
       done ;;
   esac
 done

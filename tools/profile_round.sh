@@ -18,6 +18,7 @@ step() {  # name, timeout, command...
   tail -1 "$OUT/$name.out"
 }
 PHASE=${PHASE:-all}
+ring_of() { case $1 in *int2*) echo 96 ;; *) echo 64 ;; esac; }  # bench.py WORKLOADS ring
 if [ "$PHASE" != 2 ]; then
 step bench_gemv_int4_g128 300 python bench.py
 for w in ${WORKLOADS:-gemv_int3_g64 gemv_int2_g64 gemv_int3_g64_hqq gemv_int2_g64_hqq gemm_int4_g128_m32 gemm_int4_g128_m2048 gemm_int4_g128_m65536 gemm_int4_g64_hqq_m2048}; do
@@ -32,7 +33,7 @@ find "$OUT/kt" -name "*kernel_stats.csv" -exec cp {} "$OUT/${R}_gemv_int4_g128_k
 (cd /tmp && step pmc 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run \
    -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode --no-decode-layer) || exit $?
 python tools/pmc_traffic.py "$OUT/pmc" gemv_stream gemv_int4_g128_batched \
-  "$OUT/${R}_gemv_int4_g128_batched_pmc.json"
+  "$OUT/${R}_gemv_int4_g128_batched_pmc.json" 64
 (cd /tmp && step pmc_launches 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcl" \
    -o run -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode \
    --no-decode-layer --mode launches) || exit $?
@@ -43,14 +44,14 @@ for w in gemv_int3_g64 gemv_int2_g64; do
   (cd /tmp && step pmc_$w 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_$w" -o run \
      -- python "$ROOT/bench.py" --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode \
      --no-decode-layer) || exit $?
-  python tools/pmc_traffic.py "$OUT/pmc_$w" gemv_stream ${w}_batched "$OUT/${R}_${w}_batched_pmc.json"
+  python tools/pmc_traffic.py "$OUT/pmc_$w" gemv_stream ${w}_batched "$OUT/${R}_${w}_batched_pmc.json" "$(ring_of $w)"
 done
 # the HQQ fp16-zero rings (configs[3]): FETCH_SIZE of the batched streaming launch
 for w in gemv_int3_g64_hqq gemv_int2_g64_hqq; do
   (cd /tmp && step pmc_$w 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_$w" -o run \
      -- python "$ROOT/bench.py" --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-other-mode \
      --no-decode-layer) || exit $?
-  python tools/pmc_traffic.py "$OUT/pmc_$w" gemv_stream ${w}_batched "$OUT/${R}_${w}_batched_pmc.json"
+  python tools/pmc_traffic.py "$OUT/pmc_$w" gemv_stream ${w}_batched "$OUT/${R}_${w}_batched_pmc.json" "$(ring_of $w)"
 done
 # the GEMM at configs[2] (M = 65,536): FETCH_SIZE, then the SQ passes (tools/dev/pmc_any.sh)
 (cd /tmp && step pmc_gemm65536 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_gemm" -o run \
