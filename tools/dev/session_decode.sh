@@ -1,7 +1,7 @@
 #!/bin/bash
 # Dev GPU session for decode-path changes: the attention / decode / pipeline tests (or $TESTS), the
 # bench line without the CPU baseline, and the in-graph kernel durations of the decode layers.
-# Stops at the first crash or timeout (pytest's rc 1 = failures: reported, the rest still runs).
+# Stops at the first failure, crash or timeout (a failing kernel may have faulted the GPU).
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$(pwd)
@@ -11,7 +11,7 @@ T=${TAG:-dev}
 timeout -k 10 700 python -u -m pytest ${TESTS:-tests/test_gpu_attn.py tests/test_gpu_decode.py tests/test_pipeline.py} \
   -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/${T}_tests.log" 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "passed|failed" "$OUT/${T}_tests.log" | tail -2; grep FAILED "$OUT/${T}_tests.log" | head
-[ $rc -le 1 ] || exit $rc
+[ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/${T}_bench.log" 2>&1
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 - "$OUT/${T}_bench.log" <<'PY'
