@@ -20,6 +20,7 @@ oldlib = ctypes.CDLL(os.path.join(ROOT, "tools/dev/libold.so")) if os.path.exist
 P, F = ctypes.c_void_p, ctypes.c_float
 lab.lab_wq.argtypes = [P, P, P, P, F, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                        ctypes.c_int, P, P]
+lab.lab_wqd.argtypes = lab.lab_wq.argtypes  # "wqdN": LDS-DMA ring of N chunks per wave
 N, K = int(os.environ.get("N", 28672)), int(os.environ.get("K", 4096))
 ep = qlin.EP_SILU_MUL
 ring = max(8, -(-700_000_000 // (N * K // 2)))
@@ -47,8 +48,9 @@ def run(v, qw, qsz, y, stamps=None):
                                           ctypes.c_int64(K), 4, 128, ep, st)
         assert rc == 0, rc
         return
-    rc = lab.lab_wq(P(qw.data_ptr()), P(qsz.data_ptr()), P(x.data_ptr()), P(nw16.data_ptr()),
-                    F(1e-5), P(y.data_ptr()), N, K, ep, int(v[2:]), cus,
+    fn, arg = (lab.lab_wqd, int(v[3:])) if v.startswith("wqd") else (lab.lab_wq, int(v[2:]))
+    rc = fn(P(qw.data_ptr()), P(qsz.data_ptr()), P(x.data_ptr()), P(nw16.data_ptr()),
+                    F(1e-5), P(y.data_ptr()), N, K, ep, arg, cus,
                     P(stamps.data_ptr() if stamps is not None else 0), st)
     assert rc == 0, rc
 
