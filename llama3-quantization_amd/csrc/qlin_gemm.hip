@@ -137,6 +137,94 @@ __device__ __forceinline__ void load_stage(unsigned char* st, const GemmGeo& g, 
   }
 }
 
+// KFULL (every k-tile inside K, the sources within 2 GB of their bases): the per-lane byte
+// offsets of a stage's DMA sources are formed once, and a k-tile only moves three uniform base
+// pointers — scalar adds; the checked form above spends ~39 VALU per k-tile and wave on 64-bit
+// addresses and clamps (M = 65,536 main loop: 259 VALU per 128 MFMAs)
+template <int BITS, int WN_, int GPT, int NW, bool HALF>
+struct StageOff {
+  using C = Cfg<BITS, WN_, NW, HALF>;
+  static constexpr int NX = C::BM / (4 * NW);
+  static constexpr int CH = C::RT * 16 * BITS / 64, NCH = (CH + NW - 1) / NW;
+  static constexpr int SW = C::RT * GPT * 16 / 64, NSZ = (SW + NW - 1) / NW;
+  uint32_t x[NX], c[NCH], s[NSZ > 0 ? NSZ : 1];
+};
+
+template <int BITS, int WN_, int GPT, int NW, bool HALF>
+__device__ __forceinline__ void stage_offsets(StageOff<BITS, WN_, GPT, NW, HALF>& so,
+                                              const GemmGeo& g) {
+  using C = Cfg<BITS, WN_, NW, HALF>;
+  using O = StageOff<BITS, WN_, GPT, NW, HALF>;
+  const int sub = g.lane >> 4, p = g.lane & 15;
+#pragma unroll
+  for (int j = 0; j < O::NX; ++j) {
+    const int r = (C::BM / NW) * g.wave + 4 * j + sub;
+    const int c = p ^ (r & 15);
+    const int64_t m = min(g.m0 + r, g.M - 1);
+    so.x[j] = (uint32_t)((m * g.K + 8 * c) * 2);
+  }
+#pragma unroll
+  for (int jj = 0; jj < O::NCH; ++jj) {
+    const int c = 64 * (g.wave + jj * NW) + g.lane;
+    const int rt = c / (16 * BITS), o = c % (16 * BITS);
+    const int64_t nt = min(g.nt0 + rt, g.ntl);
+    so.c[jj] = (uint32_t)((nt * g.Kt * 64 * BITS + 4 * o) * 4);
+  }
+#pragma unroll
+  for (int jj = 0; jj < O::NSZ; ++jj) {
+    const int w = 64 * (g.wave + jj * NW) + g.lane;
+    const int rt = w / (16 * GPT), i = (w / 16) % GPT, n = w & 15;
+    const int64_t nt = min(g.nt0 + rt, g.ntl);
+    so.s[jj] = (uint32_t)(((nt * g.G + i) * kTileN + n) * 4);
+  }
+}
+
+// a buffer descriptor over [p, p + 2 GB) from readfirstlane'd inputs (provably wave-uniform)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gemm_srd(const void* p) {
+  const uint64_t ad = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ad);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(ad >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7fffffff,
+                                           0x00020000);
+}
+
+struct StageSrd {
+  __amdgpu_buffer_rsrc_t x, qw, sz;
+};
+
+// the same sources as load_stage (x chunk k = kt BK + 8 c, the codes of k-tile kt, the group
+// slots of the k-tile's first group + i: a k-tile's groups are consecutive) as buffer_load ... lds
+// with the per-lane byte offset in voffset and kt's part in soffset: no VALU per k-tile
+template <int BITS, int WN_, int GPT, int NW, bool HALF>
+__device__ __forceinline__ void load_stage_kf(unsigned char* st, const GemmGeo& g, int kt,
+                                              const StageOff<BITS, WN_, GPT, NW, HALF>& so,
+                                              const StageSrd& r) {
+  using C = Cfg<BITS, WN_, NW, HALF>;
+  using O = StageOff<BITS, WN_, GPT, NW, HALF>;
+  const int xs = kt * (BK * 2), qs = kt * (64 * BITS * 4);
+  const int gs = gemm_group_of(g, kt * BK) * (kTileN * 4);
+#pragma unroll
+  for (int j = 0; j < O::NX; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        r.x, (lds_ptr)(st + ((C::BM / NW) * g.wave + 4 * j) * 256), 16, (int)so.x[j], xs, 0, 0);
+  unsigned char* bs = st + C::A_BYTES;
+#pragma unroll
+  for (int jj = 0; jj < O::NCH; ++jj) {
+    const int j = g.wave + jj * NW;  // wave-uniform
+    if (O::NCH * NW == O::CH || j < O::CH)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r.qw, (lds_ptr)(bs + 1024 * j), 16, (int)so.c[jj],
+                                               qs, 0, 0);
+  }
+  unsigned char* ss = st + C::A_BYTES + C::B_BYTES;
+#pragma unroll
+  for (int jj = 0; jj < O::NSZ; ++jj) {
+    const int j = g.wave + jj * NW;
+    if (O::NSZ * NW == O::SW || j < O::SW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r.sz, (lds_ptr)(ss + 256 * j), 4, (int)so.s[jj], gs,
+                                               0, 0);
+  }
+}
+
 // A fragments of k-step S for the wave's MB row blocks: row (lane & 15), chunk (4S + q) ^ (row & 15)
 template <int S, int MB, int WM>
 __device__ __forceinline__ void read_a(h8 (&a)[MB], const unsigned char* as, int wm, int n_in,
@@ -354,14 +442,22 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(
     kt_beg = min(split * kts, g.Kt);
     kt_end = min(kt_beg + kts, g.Kt);
   }
-  if (kt_beg < kt_end) load_stage<BITS, WN_, GPT, NW, HALF>(smem, g, kt_beg, x, qw, qsz);
+  StageOff<BITS, WN_, GPT, NW, HALF> so;
+  StageSrd srd;
+  if constexpr (KFULL) {
+    stage_offsets(so, g);
+    srd = StageSrd{gemm_srd(x), gemm_srd(qw), gemm_srd(qsz)};
+  }
+  auto stage = [&](unsigned char* st, int kt) {
+    if constexpr (KFULL) load_stage_kf<BITS, WN_, GPT, NW, HALF>(st, g, kt, so, srd);
+    else load_stage<BITS, WN_, GPT, NW, HALF>(st, g, kt, x, qw, qsz);
+  };
+  if (kt_beg < kt_end) stage(smem, kt_beg);
   for (int kt = kt_beg; kt < kt_end; ++kt) {
     // stage kt has landed for every wave, and every wave is done reading stage kt - 1
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
     __syncthreads();
-    if (!(ABL & 2) && kt + 1 < kt_end)
-      load_stage<BITS, WN_, GPT, NW, HALF>(smem + ((kt - kt_beg + 1) & 1) * C::STAGE, g, kt + 1, x,
-                                           qw, qsz);
+    if (!(ABL & 2) && kt + 1 < kt_end) stage(smem + ((kt - kt_beg + 1) & 1) * C::STAGE, kt + 1);
     if (!(ABL & 1))
       compute_stage<BITS, WN_, GPT, ZM, KFULL, NW, ABL, HALF>(smem + ((kt - kt_beg) & 1) * C::STAGE,
                                                                g, kt, acc);
@@ -417,6 +513,12 @@ uint32_t group_magic(int group) {
   return (uint32_t)(((1ull << 31) + d - 1) / d);
 }
 
+// KFULL launches address their DMA sources by 32-bit per-lane byte offsets (load_stage_kf)
+static inline bool kf_offsets_fit(int64_t M, int N, int K, int bits) {
+  const int64_t lim = (int64_t)1 << 31;
+  return M * K * 2 < lim && (int64_t)(N + 15) * K * bits / 8 < lim;
+}
+
 template <int BITS, int WN_, int GPT, int ZM, bool HALF = false>
 int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, const uint16_t* bias,
                   uint16_t* y, int64_t M, int N, int K, int group, hipStream_t st, const GemmEp& e) {
@@ -433,7 +535,7 @@ int launch_gemm_t(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x, co
                      (const _Float16*)e.res, e.ep)
   // straight-line k-steps need K % 128 == 0; the wider tiles with 2-4 group slots per k-tile then
   // spill (the per-step checks bound the scheduler), so they keep the checked form
-  if (K % BK == 0 && !(WN_ > 256 && GPT > 1)) QLIN_GL(true);
+  if (K % BK == 0 && !(WN_ > 256 && GPT > 1) && kf_offsets_fit(M, N, K, BITS)) QLIN_GL(true);
   else QLIN_GL(false);
 #undef QLIN_GL
   return (int)hipGetLastError();
@@ -491,7 +593,7 @@ int launch_gemm_split(const uint32_t* qw, const uint32_t* qsz, const uint16_t* x
                      dim3((unsigned)(tiles * S)), dim3(64 * kWaves), 0, st, qw, qsz,           \
                      (const _Float16*)x, nullptr, nullptr, M, N, K, group, group_magic(group), \
                      tiles_m, tiles_n, nullptr, 0, S, part)
-  if (K % BK == 0) QLIN_GS(true);
+  if (K % BK == 0 && kf_offsets_fit(M, N, K, BITS)) QLIN_GS(true);
   else QLIN_GS(false);
 #undef QLIN_GS
   hipLaunchKernelGGL((gemm_splitk_reduce<BITS, 128, kWaves>), dim3((unsigned)tiles),
