@@ -53,6 +53,12 @@ WORKLOADS = {
                              "int4 g128, one 2048-token PPL window"),
     "gemm_int4_g128_m65536": (65536, 4096, 4096, 4, 128, 1, "gemm",
                               "int4 g128 batch 32 x seq 2048 (configs[2], MFMA path)"),
+    # QuantLinear with act_quantizer on (quant/int_linear.py:59-60), per-token
+    # 8-bit fake-quant of x (W4A8) through qlin_linear_ep_f16 act_bits = 8
+    "gemv_int4_g128_a8": (1, 4096, 4096, 4, 128, 64, "linear_aq",
+                          "W4A8: per-token act fake-quant fused into the GEMV blocks (row f3)"),
+    "gemm_int4_g128_a8_m2048": (2048, 4096, 4096, 4, 128, 4, "linear_aq",
+                                "W4A8, one 2048-token window: act quantizer kernel + MFMA GEMM (row f3)"),
 }
 
 
@@ -594,7 +600,11 @@ def main():
     yb = torch.empty(R, M, N, device=dev, dtype=torch.float16)
     lib = qlin.load_library()
     fn = {"gemv": lib.qlin_gemv_f16, "linear": lib.qlin_linear_f16,
-          "gemm": lib.qlin_gemm_f16}[kernel]
+          "gemm": lib.qlin_gemm_f16, "linear_aq": lib.qlin_linear_ep_f16}[kernel]
+    ws, ws_bytes = None, 0
+    if kernel == "linear_aq":
+        ws_bytes = lib.qlin_linear_workspace_bytes(M, N, K, bits, group, 8)
+        ws = torch.empty(max(ws_bytes, 2) // 2, dtype=torch.float16, device=dev)
 
     def step_launches():
         st = torch.cuda.current_stream(dev).cuda_stream
@@ -603,6 +613,9 @@ def main():
             if kernel in ("gemv", "linear"):
                 rc = fn(qw.data_ptr(), qsz.data_ptr(), fl_, x.data_ptr(), None,
                         y.data_ptr(), M, N, K, bits, group, st)
+            elif kernel == "linear_aq":
+                rc = fn(qw.data_ptr(), qsz.data_ptr(), fl_, x.data_ptr(), None, None, y.data_ptr(),
+                        M, N, K, bits, group, qlin.EP_NONE, 8, 0, ws.data_ptr(), ws_bytes, st)
             else:
                 rc = fn(qw.data_ptr(), qsz.data_ptr(), fl_, x.data_ptr(), None, y.data_ptr(),
                         M, N, K, bits, group, None, 0, st)
@@ -617,7 +630,8 @@ def main():
         if rc != 0:
             raise RuntimeError(f"kernel failed: {rc}")
 
-    use_graph = not args.no_graph and kernel in ("gemv", "linear")
+    use_graph = not args.no_graph and (kernel in ("gemv", "linear") or
+                                       (kernel == "linear_aq" and M <= 64))
 
     def make_runner(step, per_graph=1):
         """One HIP graph holding `per_graph` consecutive steps (a replay = that many steps): the
@@ -757,7 +771,7 @@ def main():
         out["pipeline"] = pipeline_bench(args, dev, world, rank, backend)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(M, N, K, bits, group, args.cpu_seconds) \
-            if kernel != "gemm" else cpu_baseline(min(M, 32), N, K, bits, group, args.cpu_seconds)
+            if M <= 64 else cpu_baseline(min(M, 32), N, K, bits, group, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -69,3 +69,16 @@ def test_bench_gpus2_pipeline_leg():
     assert p["windows"]["ms_per_window"] > 0 and p["decode"]["ms_per_step"] > 0
     assert p["check"]["nll_bit_identical_to_one_process"], p["check"]
     assert p["check"]["tokens_identical_to_one_process"], p["check"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("workload,bound", [("gemv_int4_g128_a8", "hbm"),
+                                            ("gemm_int4_g128_a8_m2048", "mfma")])
+def test_bench_act_quant_workloads(workload, bound):
+    """SURVEY §8(f) row f3 measured like the other rows: the W4A8 linear (per-token 8-bit act
+    fake-quant of x, quant/int_linear.py:59-60) through qlin_linear_ep_f16 — fused into the GEMV
+    blocks at one token, the quantizer kernel + MFMA GEMM at a 2048-token window."""
+    d = _bench("--workload", workload, "--steps", "4", "--warmup", "2", "--ramp-s", "0.05",
+               "--no-cpu-baseline")
+    assert d["n_gpus"] == 1 and d["config"]["workload"] == workload
+    assert d["value"] > 0 and d["roofline"]["bound"] == bound and 0 < d["roofline"]["frac"] < 1
